@@ -1,0 +1,126 @@
+"""Speech-prompt conditioning: conformer encoder + perceiver resampler -> ``conds [B, 32, D]``.
+
+Runs once per prompt (cached by the caller, quirk Q6), so it is PyTorch-ROCm code on the device
+rather than a hand-written kernel target (§8(f) item 2 is the plan to
+move it to HIP).  Functional restatement over the reference state-dict, device agnostic.
+
+Reference behaviour followed (file:line in the reference tree):
+  * ``UnifiedVoice.get_conditioning`` conformer_perceiver branch  gpt/model.py:496-502
+  * ``BaseEncoder.forward``                                          gpt/conformer_encoder.py:400-436
+  * ``Conv2dSubsampling2.forward`` (mask ``[:, :, 2::2]``)           gpt/conformer/subsampling.py:164-190
+  * ``RelPositionalEncoding.forward`` (x*sqrt(C); pe[:, :T])        gpt/conformer/embedding.py:127-142
+  * ``ConformerEncoderLayer.forward`` (pre-LN, no macaron)          gpt/conformer_encoder.py:247-313
+  * ``RelPositionMultiHeadedAttention.forward`` (no rel_shift)       gpt/conformer/attention.py:235-312
+  * ``ConvolutionModule.forward`` (GLU, depthwise k15, LN, SiLU)     gpt/conformer_encoder.py:108-167
+  * ``PerceiverResampler.forward`` / ``Attention`` / ``Attend``       gpt/perceiver.py:263-274, 296-317, 111-150
+  * ``RMSNorm`` (F.normalize * sqrt(D) * gamma)                     gpt/perceiver.py:167-186
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def _lin(x, sd, name, bias=True):
+    return F.linear(x, sd[name + ".weight"], sd.get(name + ".bias") if bias else None)
+
+
+def _ln(x, sd, name, eps=1e-5):
+    return F.layer_norm(x, (x.shape[-1],), sd[name + ".weight"], sd[name + ".bias"], eps)
+
+
+def _rel_pos_mha(x, sd, p, heads, mask, pos_emb):
+    B, T, C = x.shape
+    dk = C // heads
+    q = _lin(x, sd, p + ".linear_q").view(B, T, heads, dk)
+    k = _lin(x, sd, p + ".linear_k").view(B, T, heads, dk).transpose(1, 2)
+    v = _lin(x, sd, p + ".linear_v").view(B, T, heads, dk).transpose(1, 2)
+    pos = F.linear(pos_emb, sd[p + ".linear_pos.weight"]).view(pos_emb.shape[0], -1, heads, dk).transpose(1, 2)
+    qu = (q + sd[p + ".pos_bias_u"]).transpose(1, 2)
+    qv = (q + sd[p + ".pos_bias_v"]).transpose(1, 2)
+    scores = (qu @ k.transpose(-2, -1) + qv @ pos.transpose(-2, -1)) / math.sqrt(dk)
+    masked = ~mask.unsqueeze(1)  # [B, 1, 1, T]
+    scores = scores.masked_fill(masked, float("-inf"))
+    attn = torch.softmax(scores, dim=-1).masked_fill(masked, 0.0)
+    out = (attn @ v).transpose(1, 2).reshape(B, T, C)
+    return _lin(out, sd, p + ".linear_out")
+
+
+def _conv_module(x, sd, p, mask):
+    C = x.shape[-1]
+    h = x.transpose(1, 2).masked_fill(~mask, 0.0)  # [B, C, T]
+    h = F.conv1d(h, sd[p + ".pointwise_conv1.weight"], sd[p + ".pointwise_conv1.bias"])
+    h = F.glu(h, dim=1)
+    w = sd[p + ".depthwise_conv.weight"]
+    h = F.conv1d(h, w, sd[p + ".depthwise_conv.bias"], padding=(w.shape[-1] - 1) // 2, groups=C)
+    h = F.silu(_ln(h.transpose(1, 2), sd, p + ".norm")).transpose(1, 2)
+    h = F.conv1d(h, sd[p + ".pointwise_conv2.weight"], sd[p + ".pointwise_conv2.bias"])
+    return h.masked_fill(~mask, 0.0).transpose(1, 2)
+
+
+def conformer_encode(sd, mel, mel_lengths, heads: int, num_blocks: int, prefix="conditioning_encoder"):
+    """mel [B, n_mels, T] -> (xs [B, T', C], mask [B, 1, T'])."""
+    x = mel.transpose(1, 2)
+    B, T, _ = x.shape
+    valid = torch.arange(T, device=x.device)[None, :] < mel_lengths.to(x.device)[:, None]
+    mask = valid.unsqueeze(1)
+    p = prefix + ".embed"
+    h = F.relu(F.conv2d(x.unsqueeze(1), sd[p + ".conv.0.weight"], sd[p + ".conv.0.bias"], stride=2))
+    b, c, t, f = h.shape
+    h = _lin(h.transpose(1, 2).reshape(b, t, c * f), sd, p + ".out.0")
+    C = h.shape[-1]
+    h = h * math.sqrt(C)
+    pos_emb = sd[p + ".pos_enc.pe"][:, :t]
+    mask = mask[:, :, 2::2]
+    for i in range(num_blocks):
+        q = f"{prefix}.encoders.{i}"
+        h = h + _rel_pos_mha(_ln(h, sd, q + ".norm_mha"), sd, q + ".self_attn", heads, mask, pos_emb)
+        h = h + _conv_module(_ln(h, sd, q + ".norm_conv"), sd, q + ".conv_module", mask)
+        y = _ln(h, sd, q + ".norm_ff")
+        h = h + _lin(F.silu(_lin(y, sd, q + ".feed_forward.w_1")), sd, q + ".feed_forward.w_2")
+        h = _ln(h, sd, q + ".norm_final")
+    return _ln(h, sd, prefix + ".after_norm"), mask
+
+
+def perceiver_resample(sd, ctx, key_mask, heads: int, prefix="perceiver_encoder"):
+    """ctx [B, T', C] + key_mask [B, 32 + T'] (True = keep) -> conds [B, 32, D]."""
+    x = _lin(ctx, sd, prefix + ".proj_context")
+    lat0 = sd[prefix + ".latents"]
+    lat = lat0.unsqueeze(0).expand(x.shape[0], -1, -1)
+    D = lat.shape[-1]
+    neg = -torch.finfo(x.dtype).max
+    for i in range(2):
+        a = f"{prefix}.layers.{i}.0"
+        context = torch.cat([lat, x], dim=1)
+        q = F.linear(lat, sd[a + ".to_q.weight"])
+        kv = F.linear(context, sd[a + ".to_kv.weight"])
+        k, v = kv.chunk(2, dim=-1)
+        B, n, inner = q.shape
+        dh = inner // heads
+        q = q.view(B, n, heads, dh).transpose(1, 2)
+        k = k.view(B, -1, heads, dh).transpose(1, 2)
+        v = v.view(B, -1, heads, dh).transpose(1, 2)
+        sim = (q @ k.transpose(-2, -1)) * (dh ** -0.5)
+        sim = sim.masked_fill(~key_mask[:, None, None, :], neg)
+        out = (sim.softmax(dim=-1) @ v).transpose(1, 2).reshape(B, n, inner)
+        lat = F.linear(out, sd[a + ".to_out.weight"]) + lat
+        f = f"{prefix}.layers.{i}.1"
+        hx, gate = _lin(lat, sd, f + ".0").chunk(2, dim=-1)
+        lat = _lin(F.gelu(gate) * hx, sd, f + ".2") + lat
+    return F.normalize(lat, dim=-1) * math.sqrt(D) * sd[prefix + ".norm.gamma"]
+
+
+def get_conditioning(sd, cfg_gpt, mel, mel_lengths=None):
+    """``UnifiedVoice.get_conditioning`` for condition_type conformer_perceiver.
+
+    mel [B, 100, T] float32 -> conds [B, 32, model_dim]."""
+    if mel.ndim == 2:
+        mel = mel.unsqueeze(0)
+    if mel_lengths is None:
+        mel_lengths = torch.full((mel.shape[0],), mel.shape[-1], dtype=torch.long, device=mel.device)
+    cm = cfg_gpt.condition_module
+    xs, mask = conformer_encode(sd, mel, mel_lengths, int(cm.attention_heads), int(cm.num_blocks))
+    key_mask = F.pad(mask.squeeze(1), (32, 0), value=True)
+    return perceiver_resample(sd, xs, key_mask, int(cm.attention_heads))

@@ -1,0 +1,213 @@
+"""ORACLE (test infrastructure only -- never imported by the product path).
+
+CPU fp32 restatement of the IndexTTS GPT speech-token path, written from the reference's math:
+prefill / KV-cached decode of the GPT-2 core, repetition-penalised greedy token selection,
+``remove_long_silence`` and the teacher-forced latent pass.  Used by ``tests/`` as the checker
+for the HIP path, by ``__graft_entry__.smoke()`` and by ``bench.py``'s ``cpu_baseline`` leg.
+
+Reference anchors (paths relative to the reference tree; ``HF:`` = transformers GPT-2, the
+third-party dependency the reference pins at 4.36.2, ``setup.py:50``):
+  * prepare_gpt_inputs (strip ids 0/1, [0]+ids+[1], left zero-pad, mask)  gpt/model.py:591-654
+  * prefill embedding = [cond;text] ++ mel_emb(8192)+mel_pos[0]         gpt/model.py:139-150
+  * decode embedding mel_emb(tok) + mel_pos[mask_len - s]  (quirk Q1)   gpt/model.py:151-155
+  * GPT-2 block: LN -> c_attn -> causal/padded SDPA (scale 1/8) -> c_proj -> +res -> LN -> c_fc ->
+    gelu_tanh -> c_proj -> +res    HF:modeling_gpt2.py:54-72,185-306 ; wpe == 0 (gpt/model.py:17-18)
+  * ln_f then final_norm then mel_head (quirk Q5)                       HF:modeling_gpt2.py:620; gpt/model.py:48,180
+  * repetition penalty over all ids incl. fake prefix (Q4); fp32 logits; first-index argmax;
+    finished rows padded with 8193                                      HF:generation/logits_process.py:409-412, utils.py:2894-2925
+  * remove_long_silence                                                  infer.py:132-186
+  * latent pass (teacher forced, positions 0..n+1, drop last 2)         gpt/model.py:521-578, 462-477
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+NEG = torch.finfo(torch.float32).min
+
+
+def _f32(sd: Dict[str, object]) -> Dict[str, torch.Tensor]:
+    return {k: torch.as_tensor(v).float() if torch.as_tensor(v).is_floating_point() else torch.as_tensor(v)
+            for k, v in sd.items()}
+
+
+class GPTOracle:
+    def __init__(self, sd, cfg_gpt):
+        self.sd = _f32(sd)
+        g = cfg_gpt
+        self.D, self.L, self.H = int(g.model_dim), int(g.layers), int(g.heads)
+        self.hd = self.D // self.H
+        self.start_text, self.stop_text = int(g.start_text_token), int(g.stop_text_token)
+        self.start_mel, self.stop_mel = int(g.start_mel_token), int(g.stop_mel_token)
+
+    # ---------------- inputs ----------------
+    def prepare_inputs(self, conds: torch.Tensor, text_ids: torch.Tensor):
+        """conds [1|B, 32, D], text_ids [B, L] -> emb [B, s, D], mask [B, s+1] (1 = attend)."""
+        sd = self.sd
+        B, L = text_ids.shape
+        ncond = conds.shape[1]
+        s = ncond + L + 2
+        emb = torch.zeros(B, s, self.D)
+        mask = torch.ones(B, s + 1, dtype=torch.long)
+        for i in range(B):
+            row = text_ids[i].long()
+            row = row[(row != self.stop_text) & (row != self.start_text)]
+            row = torch.cat([torch.tensor([self.start_text]), row, torch.tensor([self.stop_text])])
+            te = sd["text_embedding.weight"][row] + sd["text_pos_embedding.emb.weight"][: row.numel()]
+            c = conds[0] if conds.shape[0] == 1 else conds[i]
+            pad = L + 2 - row.numel()
+            emb[i, pad:] = torch.cat([c.float(), te], 0)
+            mask[i, :pad] = 0
+        return emb, mask
+
+    # ---------------- GPT-2 core ----------------
+    def _block(self, i, x, kv, attn_bias):
+        sd, H, hd = self.sd, self.H, self.hd
+        p = f"gpt.h.{i}"
+        B, T, D = x.shape
+        h = F.layer_norm(x, (D,), sd[p + ".ln_1.weight"], sd[p + ".ln_1.bias"], 1e-5)
+        qkv = torch.addmm(sd[p + ".attn.c_attn.bias"], h.reshape(-1, D), sd[p + ".attn.c_attn.weight"]).view(B, T, 3, H, hd)
+        q, k, v = (qkv[:, :, j].transpose(1, 2) for j in range(3))
+        if kv is not None:
+            if kv[i] is not None:
+                k = torch.cat([kv[i][0], k], 2)
+                v = torch.cat([kv[i][1], v], 2)
+            kv[i] = (k, v)
+        att = (q @ k.transpose(-1, -2)) * (1.0 / math.sqrt(hd)) + attn_bias
+        o = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B * T, D)
+        x = x + torch.addmm(sd[p + ".attn.c_proj.bias"], o, sd[p + ".attn.c_proj.weight"]).view(B, T, D)
+        h = F.layer_norm(x, (D,), sd[p + ".ln_2.weight"], sd[p + ".ln_2.bias"], 1e-5)
+        f = F.gelu(torch.addmm(sd[p + ".mlp.c_fc.bias"], h.reshape(-1, D), sd[p + ".mlp.c_fc.weight"]), approximate="tanh")
+        return x + torch.addmm(sd[p + ".mlp.c_proj.bias"], f, sd[p + ".mlp.c_proj.weight"]).view(B, T, D)
+
+    def core(self, x, attn_bias, kv=None):
+        for i in range(self.L):
+            x = self._block(i, x, kv, attn_bias)
+        return F.layer_norm(x, (self.D,), self.sd["gpt.ln_f.weight"], self.sd["gpt.ln_f.bias"], 1e-5)
+
+    def head(self, h):
+        sd = self.sd
+        h = F.layer_norm(h, (self.D,), sd["final_norm.weight"], sd["final_norm.bias"], 1e-5)
+        return F.linear(h, sd["mel_head.weight"], sd["mel_head.bias"])
+
+    @staticmethod
+    def _bias(mask_keys: torch.Tensor, q_len: int):
+        """additive [B, 1, q_len, K] bias: causal over the last q_len keys + key padding."""
+        B, K = mask_keys.shape
+        qpos = torch.arange(K - q_len, K)[:, None]
+        causal = torch.arange(K)[None, :] <= qpos
+        ok = causal[None] & mask_keys.bool()[:, None, :]
+        return torch.where(ok, 0.0, NEG)[:, None]
+
+    # ---------------- token selection ----------------
+    @staticmethod
+    def penalize(logits: torch.Tensor, seen: torch.Tensor, penalty: float):
+        """``RepetitionPenaltyLogitsProcessor``: x<0 ? x*p : x/p at every id already in the sequence."""
+        pen = torch.where(logits < 0, logits * penalty, logits / penalty)
+        return torch.where(seen, pen, logits)
+
+    def generate(self, conds, text_ids, max_new_tokens: int, repetition_penalty: float = 10.0,
+                 min_new_tokens: int = 0, return_trace: bool = False):
+        """Greedy decode (do_sample=False, num_beams=1).  -> codes [B, n] (finished rows padded 8193)."""
+        emb, mask = self.prepare_inputs(conds, text_ids)
+        B, s, D = emb.shape
+        sd = self.sd
+        V = sd["mel_head.weight"].shape[0]
+        start = sd["mel_embedding.weight"][self.start_mel] + sd["mel_pos_embedding.emb.weight"][0]
+        x = torch.cat([emb, start.expand(B, 1, D)], 1)
+        kv: List[Optional[tuple]] = [None] * self.L
+        h = self.core(x, self._bias(mask, s + 1), kv)
+        logits = self.head(h[:, -1])
+        seen = torch.zeros(B, V, dtype=torch.bool)
+        seen[:, 1] = True  # the fake prefix ids (gpt/model.py:645-653)
+        seen[:, self.start_mel] = True
+        done = torch.zeros(B, dtype=torch.bool)
+        out, trace = [], []
+        for step in range(max_new_tokens):
+            sc = self.penalize(logits, seen, repetition_penalty)
+            if step < min_new_tokens:
+                sc[:, self.stop_mel] = float("-inf")
+            if return_trace:
+                top2 = torch.topk(sc, 2, dim=-1)
+                trace.append((sc.clone(), top2.values[:, 0] - top2.values[:, 1]))
+            nxt = torch.argmax(sc, dim=-1)
+            nxt = torch.where(done, torch.full_like(nxt, self.stop_mel), nxt)
+            out.append(nxt)
+            seen[torch.arange(B), nxt] = True
+            done |= nxt == self.stop_mel
+            if bool(done.all()):
+                break
+            mask = torch.cat([mask, torch.ones(B, 1, dtype=mask.dtype)], 1)
+            pos = mask.shape[1] - s  # quirk Q1: position j+1 for the j-th fed-back token (j >= 1)
+            e = sd["mel_embedding.weight"][nxt] + sd["mel_pos_embedding.emb.weight"][pos]
+            h = self.core(e[:, None], self._bias(mask, 1), kv)
+            logits = self.head(h[:, -1])
+        codes = torch.stack(out, 1)
+        return (codes, trace) if return_trace else codes
+
+    def forced_logits(self, conds, text_ids, codes: torch.Tensor):
+        """Teacher-forced decode: the logits (after penalty) the generate loop sees at each step when
+        fed ``codes`` -> [B, n, V]. Lets fixtures compare per-step logits without free-running drift."""
+        emb, mask = self.prepare_inputs(conds, text_ids)
+        B, s, D = emb.shape
+        sd = self.sd
+        start = sd["mel_embedding.weight"][self.start_mel] + sd["mel_pos_embedding.emb.weight"][0]
+        x = torch.cat([emb, start.expand(B, 1, D)], 1)
+        n = codes.shape[1]
+        pos = torch.tensor([0] + list(range(2, n + 1)))  # positions 0, 2, 3, ... (Q1)
+        tok = codes[:, : n - 1]
+        e = sd["mel_embedding.weight"][tok] + sd["mel_pos_embedding.emb.weight"][pos[1:n]][None]
+        full = torch.cat([x, e], 1)
+        mask_full = torch.cat([mask, torch.ones(B, n - 1, dtype=mask.dtype)], 1)
+        h = self.core(full, self._bias(mask_full, full.shape[1]))
+        return self.head(h[:, s:])
+
+    # ---------------- post-processing + latent pass ----------------
+    @staticmethod
+    def remove_long_silence(codes: torch.Tensor, stop_mel: int = 8193, silent_token: int = 52, max_consecutive: int = 30):
+        lens, rows, fixed = [], [], False
+        for i in range(codes.shape[0]):
+            c = codes[i]
+            hits = (c == stop_mel).nonzero()
+            n = int(hits[0]) if len(hits) else c.numel()
+            if int((c == silent_token).sum()) > max_consecutive:
+                keep, run = [], 0
+                for k in range(n):
+                    if int(c[k]) != silent_token:
+                        keep.append(k)
+                        run = 0
+                    elif run < 10:
+                        keep.append(k)
+                        run += 1
+                rows.append(c[keep])
+                n = len(keep)
+                fixed = True
+            else:
+                rows.append(c[:n])
+            lens.append(n)
+        if fixed:
+            codes = torch.nn.utils.rnn.pad_sequence(rows, batch_first=True, padding_value=stop_mel) if len(rows) > 1 \
+                else rows[0][None]
+        m = max(lens)
+        return codes[:, :m], torch.tensor(lens, dtype=torch.long)
+
+    def latent(self, conds, text_ids, codes):
+        """``UnifiedVoice.forward(..., return_latent=True)`` for ONE utterance (B=1, no padding).
+
+        conds [1, 32, D]; text_ids [1, L] (as given; no 0/1 stripping on this path);
+        codes [1, n] -> latent [1, n, D]."""
+        sd = self.sd
+        t = torch.cat([torch.tensor([[self.start_text]]), text_ids.long(), torch.tensor([[self.stop_text]])], 1)
+        # gpt/model.py:559-566: text padded with stop (already full length), mel padded with stop
+        m = torch.cat([torch.tensor([[self.start_mel]]), codes.long(), torch.tensor([[self.stop_mel]])], 1)
+        # set_mel_padding: code_lens*1024 -> ceil(.)+1 >= n, so no in-range position is replaced
+        te = sd["text_embedding.weight"][t] + sd["text_pos_embedding.emb.weight"][: t.shape[1]][None]
+        me = sd["mel_embedding.weight"][m] + sd["mel_pos_embedding.emb.weight"][: m.shape[1]][None]
+        x = torch.cat([conds.float(), te, me], 1)
+        T = x.shape[1]
+        h = self.core(x, self._bias(torch.ones(1, T), T))
+        h = F.layer_norm(h[:, conds.shape[1]:], (self.D,), sd["final_norm.weight"], sd["final_norm.bias"], 1e-5)
+        return h[:, -m.shape[1]:][:, :-2]
