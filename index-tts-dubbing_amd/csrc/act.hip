@@ -1,0 +1,157 @@
+// Fused anti-aliased SnakeBeta activation (BigVGAN Activation1d) for gfx950.
+//
+// Replaces the reference's native op anti_alias_activation_cuda.forward
+// (indextts/BigVGAN/alias_free_activation/cuda/anti_alias_activation.cpp:19-23) but follows the
+// semantics of the *torch* path (alias_free_torch/act.py:24-29, resample.py:25-49, quirk Q7):
+//   u[2p]   = 2 * sum_{q=-3..2} x[clamp(p+q)] * f[5-2q]        (replicate pad 5, 2x conv_transpose, crop 15)
+//   u[2p+1] = 2 * sum_{q=-2..3} x[clamp(p+q)] * f[6-2q]
+//   v[m]    = u[m] + 1/(exp(b)+1e-9) * sin(u[m]*exp(a))^2       (SnakeBeta, log-scale a/b)
+//   y[t]    = sum_{k=0..11} g[k] * v[clamp(2t+k-5, 0, 2L-1)]    (replicate pad 5/6, stride-2 low-pass)
+// where clamp() is per utterance length L (ragged batches are exact: every utterance sees its own edges).
+//
+// Layout: any strides (the vocoder uses channel-last [B, T, C]; the reference op is [B, C, T]).
+// One workgroup = 256 threads = a [TT x CT] (time x channel) output tile; the raw input window
+// [TT+12 x CT] is staged once through LDS as f32 (replicate-clamped rows), then each thread runs a
+// 16-output register window along time for one channel (HBM-bound: 1 read + 1 write per element).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTO = 16;   // outputs per thread along time
+constexpr int kHalo = 6;  // input samples each side that one output depends on
+
+struct ActArgs {
+  const void* x;
+  void* y;
+  const float* up;
+  const float* down;
+  const float* log_alpha;
+  const float* log_beta;
+  const int32_t* lens;
+  int B, C, T, CT, nsub;
+  int64_t sxb, sxt, sxc, syb, syt, syc;
+};
+
+__device__ __forceinline__ float snake(float u, float a, float inv_b) {
+  float s = sinf(u * a);
+  return u + inv_b * (s * s);
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int b = blockIdx.z;
+  const int CT = p.CT, nsub = p.nsub, TT = nsub * kTO;
+  const int t0 = blockIdx.x * TT;
+  const int c0 = blockIdx.y * CT;
+  const int len = p.lens ? p.lens[b] : p.T;
+  if (t0 >= len) return;  // uniform per block
+  const TI* x = reinterpret_cast<const TI*>(p.x) + (int64_t)b * p.sxb;
+  TO* y = reinterpret_cast<TO*>(p.y) + (int64_t)b * p.syb;
+
+  const int rows = TT + 2 * kHalo;
+  for (int idx = threadIdx.x; idx < rows * CT; idx += kThreads) {
+    int r = idx / CT, c = idx - r * CT;
+    int t = min(max(t0 - kHalo + r, 0), len - 1);
+    int ch = c0 + c;
+    xs[idx] = ch < p.C ? St<TI>::ld(x + (int64_t)t * p.sxt + (int64_t)ch * p.sxc) : 0.f;
+  }
+  __syncthreads();
+
+  const int c = threadIdx.x % CT, sub = threadIdx.x / CT;
+  const int ch = c0 + c;
+  if (sub >= nsub || ch >= p.C) return;
+  const int ts = t0 + sub * kTO;
+  if (ts >= len) return;
+  float f[12], g[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) { f[k] = p.up[k]; g[k] = p.down[k]; }
+  const float a = expf(p.log_alpha[ch]);
+  const float inv_b = 1.0f / (expf(p.log_beta[ch]) + 1e-9f);
+  const float* col = xs + (sub * kTO) * CT + c;  // row r <-> t = ts - 6 + r
+
+  if (ts >= 3 && ts + kTO + 3 <= len) {
+    float xr[kTO + 2 * kHalo];
+#pragma unroll
+    for (int i = 0; i < kTO + 2 * kHalo; ++i) xr[i] = col[i * CT];
+    float v[2 * kTO + 10];
+#pragma unroll
+    for (int j = 0; j < 2 * kTO + 10; ++j) {
+      float acc = 0.f;
+      if (j & 1) {  // even upsampled index
+#pragma unroll
+        for (int q = -3; q <= 2; ++q) acc = fmaf(xr[4 + (j - 1) / 2 + q], f[5 - 2 * q], acc);
+      } else {
+#pragma unroll
+        for (int q = -2; q <= 3; ++q) acc = fmaf(xr[3 + j / 2 + q], f[6 - 2 * q], acc);
+      }
+      v[j] = snake(2.0f * acc, a, inv_b);
+    }
+#pragma unroll
+    for (int i = 0; i < kTO; ++i) {
+      float o = 0.f;
+#pragma unroll
+      for (int k = 0; k < 12; ++k) o = fmaf(g[k], v[2 * i + k], o);
+      St<TO>::st(y + (int64_t)(ts + i) * p.syt + (int64_t)ch * p.syc, o);
+    }
+  } else {
+    // edge chunk: explicit two-level replicate clamping (x level and activated-signal level)
+    const int base = ts - kHalo;  // t of LDS row `sub*kTO`
+    const int te = min(ts + kTO, len);
+    for (int t = ts; t < te; ++t) {
+      float o = 0.f;
+      for (int k = 0; k < 12; ++k) {
+        int m = min(max(2 * t + k - 5, 0), 2 * len - 1);
+        int pp = m >> 1;
+        float acc = 0.f;
+        if ((m & 1) == 0) {
+          for (int q = -3; q <= 2; ++q) acc = fmaf(col[(min(max(pp + q, 0), len - 1) - base) * CT], f[5 - 2 * q], acc);
+        } else {
+          for (int q = -2; q <= 3; ++q) acc = fmaf(col[(min(max(pp + q, 0), len - 1) - base) * CT], f[6 - 2 * q], acc);
+        }
+        o = fmaf(g[k], snake(2.0f * acc, a, inv_b), o);
+      }
+      St<TO>::st(y + (int64_t)t * p.syt + (int64_t)ch * p.syc, o);
+    }
+  }
+}
+
+template <typename TI, typename TO>
+void launch(const ActArgs& a, hipStream_t s) {
+  dim3 grid((a.T + a.nsub * kTO - 1) / (a.nsub * kTO), (a.C + a.CT - 1) / a.CT, a.B);
+  size_t lds = sizeof(float) * (size_t)(a.nsub * kTO + 2 * kHalo) * a.CT;
+  hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO>), grid, dim3(kThreads), lds, s, a);
+}
+
+}  // namespace
+
+extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, const float* down12,
+                                     const float* log_alpha, const float* log_beta, const int32_t* lengths,
+                                     int B, int C, int T, int64_t x_sb, int64_t x_st, int64_t x_sc, int64_t y_sb,
+                                     int64_t y_st, int64_t y_sc, int dtype_in, int dtype_out, void* stream) {
+  const char* fn = "itts_aa_snakebeta_fwd";
+  ITTS_REQUIRE(B >= 0 && C >= 0 && T >= 0, fn, "negative size");
+  if (B == 0 || C == 0 || T == 0) return 0;
+  ITTS_REQUIRE(x && y && up12 && down12 && log_alpha && log_beta, fn, "null pointer");
+  ITTS_REQUIRE((dtype_in == ITTS_F32 || dtype_in == ITTS_BF16) && (dtype_out == ITTS_F32 || dtype_out == ITTS_BF16),
+               fn, "unsupported dtype (f32=0, bf16=1)");
+  ActArgs a{x, y, up12, down12, log_alpha, log_beta, lengths, B, C, T, 0, 0, x_sb, x_st, x_sc, y_sb, y_st, y_sc};
+  a.CT = C < 64 ? C : 64;
+  a.nsub = kThreads / a.CT;
+  hipStream_t s = itts::as_stream(stream);
+  if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, s);
+  else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, s);
+  else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, s);
+  else launch<uint16_t, float>(a, s);
+  return itts::check_launch(fn);
+}
+
+// Drop-in for the reference's contiguous [B, C, T] op (anti_alias_activation_cuda.forward),
+// with caller-owned output (torch-path edge semantics, see header).
+extern "C" int itts_aa_snakebeta_bct(const void* x, void* y, const float* up12, const float* down12,
+                                     const float* log_alpha, const float* log_beta, int B, int C, int T, int dtype,
+                                     void* stream) {
+  return itts_aa_snakebeta_fwd(x, y, up12, down12, log_alpha, log_beta, nullptr, B, C, T, (int64_t)C * T, 1, T,
+                               (int64_t)C * T, 1, T, dtype, dtype, stream);
+}

@@ -1,0 +1,58 @@
+// Shared device/host helpers for libitts_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
+
+enum ItTsDtype { ITTS_F32 = 0, ITTS_BF16 = 1 };
+
+// ---- bf16 <-> f32 (bf16 carried as raw uint16_t) ----
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);  // round to nearest even (NaN payloads may collapse: not produced here)
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+// Storage-type traits: every kernel computes in f32 and loads/stores T.
+template <typename T> struct St;
+template <> struct St<float> {
+  __device__ __forceinline__ static float ld(const float* p) { return *p; }
+  __device__ __forceinline__ static void st(float* p, float v) { *p = v; }
+};
+template <> struct St<uint16_t> {
+  __device__ __forceinline__ static float ld(const uint16_t* p) { return bf2f(*p); }
+  __device__ __forceinline__ static void st(uint16_t* p, float v) { *p = f2bf(v); }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- host-side error plumbing (no C++ exception crosses the C ABI) ----
+namespace itts {
+void set_error(const std::string& msg);
+int fail(const char* fn, const char* what);
+int check_launch(const char* fn);
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+}  // namespace itts
+
+#define ITTS_REQUIRE(cond, fn, what) \
+  do {                               \
+    if (!(cond)) return itts::fail(fn, what); \
+  } while (0)

@@ -1,0 +1,251 @@
+// Implicit-GEMM on MFMA (v_mfma_f32_32x32x16_bf16) for gfx950: one kernel serves
+//   * BigVGAN Conv1d (dilated, zero "same" padding)      BigVGAN/models.py:24-42, utils.py:59-60
+//   * BigVGAN ConvTranspose1d as u polyphase convs        BigVGAN/models.py:155-161 (torch ConvTranspose1d)
+//   * conv_pre                                             BigVGAN/models.py:149,224
+//   * GPT-2 projection GEMMs for prefill + latent pass     HF:modeling_gpt2.py Conv1D = addmm(b, x, W)
+//
+//   Y[b, q*ymul + yoff, n] = epi( sum_j sum_c  X[b, q + tap_off[j], c] * Wp[j][n][c] )
+// with X rows outside [0, len_b) reading as zero (per-utterance zero padding, so ragged batches are
+// exact).  Layout is channel-last: X [B][Tmax][ldx] bf16, Y [B][Tout][ldy] (bf16 or f32).
+// Wp is prepacked on the host: [ntaps][co_pad][ci_pad] bf16, zero padded.
+//
+// Epilogue: v = acc + bias[n] + bias_b[b][n]; if gelu: v = gelu_tanh(v); v = alpha*(v + r1 + r2)
+// (r1/r2 residual tensors with Y's layout and dtype; r1 may alias Y).
+//
+// Tiling: 256 threads = 4 waves; block tile TM x TN, K step KC (channels of one tap) staged
+// through double-buffered LDS (row pitch padded by 16 B -> conflict-free ds_read_b128 fragments),
+// next K-step's global loads issued into registers before the current step's MFMAs.
+#include "common.h"
+
+namespace {
+
+constexpr int kMaxTaps = 16;
+
+struct IgArgs {
+  const uint16_t* x;
+  const uint16_t* w;
+  const float* bias;
+  const float* bias_b;
+  const void* r1;
+  const void* r2;
+  void* y;
+  const int32_t* lens;
+  int B, Tmax, Cin, Cout, ci_pad, co_pad, ntaps;
+  int64_t sxb, ldx, syb, ldy;
+  int ymul, yoff;
+  float alpha;
+  int gelu;
+  int tap_off[kMaxTaps];
+};
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+template <int TM, int TN, int WM, int WN, int KC, bool VEC, typename OutT>
+__global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
+  constexpr int PITCH = KC * 2 + 16;            // bytes per LDS row
+  constexpr int A_BYTES = TM * PITCH, B_BYTES = TN * PITCH;
+  constexpr int VPR = KC / 8;                   // 16-B vectors per row
+  constexpr int A_TOT = TM * VPR, B_TOT = TN * VPR;  // 16-B vectors per tile
+  constexpr int A_VEC = (A_TOT + 255) / 256, B_VEC = (B_TOT + 255) / 256;
+  constexpr int FM = WM / 32, FN = WN / 32;     // MFMA tiles per wave
+  constexpr int WAVES_N = TN / WN;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int b = blockIdx.z;
+  const int len = p.lens ? p.lens[b] : p.Tmax;
+  const int q0 = blockIdx.x * TM;
+  if (q0 >= len) return;
+  const int n0 = blockIdx.y * TN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const uint16_t* X = p.x + (int64_t)b * p.sxb;
+  const int nchunks = p.ci_pad / KC;
+  const int kiters = p.ntaps * nchunks;
+
+  u32x4_t ra[A_VEC], rb[B_VEC];
+  auto gload = [&](int it) {
+    const int j = it / nchunks, c0 = (it - j * nchunks) * KC;
+    const int toff = p.tap_off[j];
+#pragma unroll
+    for (int i = 0; i < A_VEC; ++i) {
+      const int v = tid + 256 * i, row = v / VPR, cv = (v % VPR) * 8;
+      const int t = q0 + row + toff, c = c0 + cv;
+      u32x4_t val = {0u, 0u, 0u, 0u};
+      if (v < A_TOT && t >= 0 && t < len) {
+        const uint16_t* src = X + (int64_t)t * p.ldx + c;
+        if (VEC) {
+          if (c < p.Cin) val = *reinterpret_cast<const u32x4_t*>(src);
+        } else {
+          uint32_t e[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) e[u] = (c + u < p.Cin) ? src[u] : 0u;
+          val = u32x4_t{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
+        }
+      }
+      ra[i] = val;
+    }
+    const uint16_t* Wj = p.w + ((int64_t)j * p.co_pad + n0) * p.ci_pad + c0;
+#pragma unroll
+    for (int i = 0; i < B_VEC; ++i) {
+      const int v = tid + 256 * i, row = v / VPR, cv = (v % VPR) * 8;
+      if (v < B_TOT) rb[i] = *reinterpret_cast<const u32x4_t*>(Wj + (int64_t)row * p.ci_pad + cv);
+    }
+  };
+  auto swrite = [&](int buf) {
+    unsigned char* As = smem + buf * (A_BYTES + B_BYTES);
+    unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_VEC; ++i) {
+      const int v = tid + 256 * i, row = v / VPR, cv = v % VPR;
+      if (v < A_TOT) *reinterpret_cast<u32x4_t*>(As + row * PITCH + cv * 16) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_VEC; ++i) {
+      const int v = tid + 256 * i, row = v / VPR, cv = v % VPR;
+      if (v < B_TOT) *reinterpret_cast<u32x4_t*>(Bs + row * PITCH + cv * 16) = rb[i];
+    }
+  };
+
+  f32x16_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int it = 0; it < kiters; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < kiters) gload(it + 1);
+    const unsigned char* As = smem + buf * (A_BYTES + B_BYTES);
+    const unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < KC / 16; ++ks) {
+      bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(As + (wm + 32 * i + r32) * PITCH + ks * 32 + h * 16);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn + 32 * j + r32) * PITCH + ks * 32 + h * 16);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (it + 1 < kiters) {
+      swrite(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: lane holds column n = wn + 32j + (lane&31); rows (r&3) + 8(r>>2) + 4h
+  OutT* Y = reinterpret_cast<OutT*>(p.y) + (int64_t)b * p.syb;
+  const OutT* R1 = reinterpret_cast<const OutT*>(p.r1);
+  const OutT* R2 = reinterpret_cast<const OutT*>(p.r2);
+  if (R1) R1 += (int64_t)b * p.syb;
+  if (R2) R2 += (int64_t)b * p.syb;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn + 32 * j + r32;
+    if (n >= p.Cout) continue;
+    float bn = p.bias ? p.bias[n] : 0.f;
+    if (p.bias_b) bn += p.bias_b[(int64_t)b * p.Cout + n];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = q0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (q >= len) continue;
+        const int64_t off = (int64_t)(q * p.ymul + p.yoff) * p.ldy + n;
+        float v = acc[i][j][r] + bn;
+        if (p.gelu) v = gelu_tanh(v);
+        if (R1) v += St<OutT>::ld(R1 + off);
+        if (R2) v += St<OutT>::ld(R2 + off);
+        St<OutT>::st(Y + off, p.alpha * v);
+      }
+    }
+  }
+}
+
+template <int TM, int TN, int WM, int WN, int KC, typename OutT>
+void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
+  dim3 grid((a.Tmax + TM - 1) / TM, (a.Cout + TN - 1) / TN, a.B);
+  size_t lds = 2 * (size_t)(TM + TN) * (KC * 2 + 16);
+  if (vec)
+    hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, false, OutT>), grid, dim3(256), lds, s, a);
+}
+
+template <typename OutT>
+void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
+  const bool wide_n = a.Cout >= 128, wide_k = a.Cin >= 128;
+  if (wide_n && wide_k) launch_cfg<128, 128, 64, 64, 64, OutT>(a, vec, s);
+  else if (wide_n) launch_cfg<128, 128, 64, 64, 32, OutT>(a, vec, s);
+  else if (wide_k) launch_cfg<128, 32, 32, 32, 64, OutT>(a, vec, s);
+  else launch_cfg<128, 32, 32, 32, 32, OutT>(a, vec, s);
+}
+
+}  // namespace
+
+// Packing contract for Wp: ci_pad = round_up(Cin, Cin >= 128 ? 64 : 32),
+// co_pad = round_up(Cout, Cout >= 128 ? 128 : 32).
+extern "C" int itts_igemm_pack_dims(int Cin, int Cout, int* ci_pad, int* co_pad) {
+  if (!ci_pad || !co_pad || Cin <= 0 || Cout <= 0) return itts::fail("itts_igemm_pack_dims", "bad args");
+  const int kc = Cin >= 128 ? 64 : 32, tn = Cout >= 128 ? 128 : 32;
+  *ci_pad = (Cin + kc - 1) / kc * kc;
+  *co_pad = (Cout + tn - 1) / tn * tn;
+  return 0;
+}
+
+extern "C" int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, const float* bias,
+                              const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy,
+                              const int32_t* lengths, int B, int Tmax, int Cin, int Cout, int ntaps,
+                              const int32_t* tap_off, int y_row_mul, int y_row_off, float alpha, int gelu,
+                              int out_dtype, void* stream) {
+  const char* fn = "itts_igemm_fwd";
+  ITTS_REQUIRE(B >= 0 && Tmax >= 0 && Cin > 0 && Cout > 0, fn, "bad sizes");
+  if (B == 0 || Tmax == 0) return 0;
+  ITTS_REQUIRE(ntaps >= 1 && ntaps <= kMaxTaps, fn, "ntaps must be in [1, 16]");
+  ITTS_REQUIRE(x && w_packed && y && tap_off, fn, "null pointer");
+  ITTS_REQUIRE(out_dtype == ITTS_F32 || out_dtype == ITTS_BF16, fn, "out dtype must be f32 (0) or bf16 (1)");
+  ITTS_REQUIRE(y_row_mul >= 1 && y_row_off >= 0, fn, "bad output row mapping");
+  IgArgs a{};
+  a.x = static_cast<const uint16_t*>(x);
+  a.w = static_cast<const uint16_t*>(w_packed);
+  a.bias = bias;
+  a.bias_b = bias_b;
+  a.r1 = r1;
+  a.r2 = r2;
+  a.y = y;
+  a.lens = lengths;
+  a.B = B;
+  a.Tmax = Tmax;
+  a.Cin = Cin;
+  a.Cout = Cout;
+  itts_igemm_pack_dims(Cin, Cout, &a.ci_pad, &a.co_pad);
+  a.ntaps = ntaps;
+  a.sxb = x_sb;
+  a.ldx = ldx;
+  a.syb = y_sb;
+  a.ldy = ldy;
+  a.ymul = y_row_mul;
+  a.yoff = y_row_off;
+  a.alpha = alpha;
+  a.gelu = gelu;
+  for (int j = 0; j < ntaps; ++j) a.tap_off[j] = tap_off[j];
+  const bool vec = (Cin % 8 == 0) && (ldx % 8 == 0) && (x_sb % 8 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  hipStream_t s = itts::as_stream(stream);
+  if (out_dtype == ITTS_BF16) dispatch<uint16_t>(a, vec, s);
+  else dispatch<float>(a, vec, s);
+  return itts::check_launch(fn);
+}

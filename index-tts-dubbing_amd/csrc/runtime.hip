@@ -1,0 +1,31 @@
+// C-ABI runtime plumbing for libitts_hip: thread-local error strings, launch checks, version.
+#include <cstdio>
+
+#include "common.h"
+
+namespace itts {
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(const char* fn, const char* what) {
+  set_error(std::string(fn) + ": " + what);
+  return -1;
+}
+
+int check_launch(const char* fn) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(fn) + ": " + hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}
+}  // namespace itts
+
+extern "C" const char* itts_last_error(void) { return itts::g_last_error.c_str(); }
+
+extern "C" int itts_abi_version(void) { return 1; }
+
+// Which gfx target this code object was built for (sanity check from the host).
+extern "C" const char* itts_build_target(void) { return "gfx950"; }

@@ -1,0 +1,102 @@
+"""ctypes binding of libitts_hip.so -- the C-ABI boundary of the HIP hot path (include/itts_hip.h).
+
+The library is built in-tree (``indextts/_build.py``; ``__graft_entry__.build()``) for gfx950 and
+loaded AFTER ``import torch`` so it binds torch's already-loaded ``libamdhip64.so.7`` (same soname
+as ROCm 7.2's), i.e. one HIP runtime per process.  There is no fallback: if the library is missing
+or a call fails, a ``RuntimeError`` is raised (the reference's loader silently fell back to torch,
+``indextts/infer.py:97-109``; here the HIP path is the product).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported first: provides the HIP runtime)
+
+LIB_NAME = "libitts_hip.so"
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG_DIR, LIB_NAME)
+
+F32, BF16 = 0, 1
+
+_c_i = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_f = ctypes.c_float
+_vp = ctypes.c_void_p
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+# name -> (restype, argtypes); keep in sync with include/itts_hip.h
+SIGNATURES = {
+    "itts_last_error": (ctypes.c_char_p, []),
+    "itts_abi_version": (_c_i, []),
+    "itts_build_target": (ctypes.c_char_p, []),
+    "itts_aa_snakebeta_fwd": (_c_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_i64, _c_i64, _c_i64,
+                                     _c_i64, _c_i64, _c_i64, _c_i, _c_i, _vp]),
+    "itts_aa_snakebeta_bct": (_c_i, [_vp, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_i, _vp]),
+    "itts_igemm_pack_dims": (_c_i, [_c_i, _c_i, _i32p, _i32p]),
+    "itts_igemm_fwd": (_c_i, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i, _c_i,
+                              _c_i, _c_i, _c_i, _i32p, _c_i, _c_i, _c_f, _c_i, _c_i, _vp]),
+    "itts_conv_post_tanh": (_c_i, [_vp, _c_i64, _c_i64, _vp, _c_f, _c_i, _c_i, _vp, _c_i, _c_i, _vp, _vp, _c_i64,
+                                   _c_i, _vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def load(path: str = None):
+    """Load (once) and return the ctypes library; raises if it is absent or incomplete."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or os.environ.get("ITTS_HIP_LIB", LIB_PATH)
+        if not os.path.exists(p):
+            raise HipError(f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)  # AttributeError = stale library
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        msg = _lib.itts_last_error().decode(errors="replace") if _lib else ""
+        raise HipError(f"{name} failed (rc={rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(t) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise HipError(f"unsupported dtype {t.dtype}")
+
+
+def i32_array(vals):
+    arr = (ctypes.c_int32 * len(vals))(*[int(v) for v in vals])
+    return arr

@@ -1,0 +1,247 @@
+"""BigVGAN2 vocoder on the HIP C-ABI (speech-code latents -> 24 kHz waveform).
+
+Mirrors ``BigVGAN.forward`` (reference ``indextts/BigVGAN/models.py:201-250``) for a whole batch of
+utterances at once, with per-utterance lengths (ragged batches are exact: every conv and
+activation clamps/zero-pads at each utterance's own edges, as if it ran alone at batch 1 like the
+reference's ``infer()``).
+
+HBM layout: channel-last ``[B, T_stage, C]`` bf16 activations (T_stage = T * prod(upsample rates so
+far)); weights prepacked once as bf16 ``[taps][co_pad][ci_pad]`` for the MFMA implicit-GEMM kernel.
+Per stage:  ConvTranspose1d (u polyphase launches; + conds[i](spk) as a per-utterance bias)
+            -> 3 AMPBlock1, each 3 x [act -> conv(dil) -> act -> conv + residual]; the third conv of
+               each block also accumulates the block sum and applies the 1/3 mean in its epilogue.
+Tail: activation_post -> conv_post + tanh (+ int16 conversion of ``infer()``) in one kernel.
+
+The speaker embedding (ECAPA) and the per-utterance condition biases are per-prompt work done with
+PyTorch ops on the device and cached by the caller (quirk Q6).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .. import _hip
+from .ecapa import speaker_embedding
+
+
+def fold_weight_norm(sd) -> Dict[str, torch.Tensor]:
+    """``remove_weight_norm``: w = g * v / ||v|| with the norm over every dim but 0 (f32)."""
+    out = {}
+    for k, v in sd.items():
+        t = torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor) else v
+        if k.endswith(".weight_g"):
+            continue
+        if k.endswith(".weight_v"):
+            base = k[: -len(".weight_v")]
+            g = torch.as_tensor(np.asarray(sd[base + ".weight_g"])).float() if not isinstance(sd[base + ".weight_g"], torch.Tensor) \
+                else sd[base + ".weight_g"].float()
+            vv = t.float()
+            n = vv.reshape(vv.shape[0], -1).norm(dim=1).reshape(g.shape)
+            out[base + ".weight"] = g * vv / n
+        else:
+            out[k] = t.float() if t.is_floating_point() else t
+    return out
+
+
+def pack_dims(cin: int, cout: int):
+    """itts_igemm_pack_dims through the C ABI."""
+    lib = _hip.load()
+    ci, co = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    ci_p = ci.ctypes.data_as(_hip._i32p)
+    co_p = co.ctypes.data_as(_hip._i32p)
+    _hip.check(lib.itts_igemm_pack_dims(cin, cout, ci_p, co_p), "itts_igemm_pack_dims")
+    return int(ci[0]), int(co[0])
+
+
+def pack_dims_py(cin: int, cout: int):
+    """Same contract as itts_igemm_pack_dims (used where the library is not loaded, e.g. CPU tests)."""
+    kc = 64 if cin >= 128 else 32
+    tn = 128 if cout >= 128 else 32
+    return (cin + kc - 1) // kc * kc, (cout + tn - 1) // tn * tn
+
+
+def pack_taps(taps: List[torch.Tensor], cin: int, cout: int) -> torch.Tensor:
+    """taps: list of [cout, cin] f32 matrices -> bf16 [ntaps, co_pad, ci_pad] (zero padded)."""
+    ci_pad, co_pad = pack_dims_py(cin, cout)
+    out = torch.zeros(len(taps), co_pad, ci_pad, dtype=torch.float32)
+    for j, w in enumerate(taps):
+        out[j, :cout, :cin] = w
+    return out.to(torch.bfloat16)
+
+
+def conv1d_taps(w: torch.Tensor, dilation: int = 1, padding: int = None):
+    """Conv1d weight [co, ci, k] -> (tap matrices, time offsets): y[t] = sum_j W_j x[t + off_j]."""
+    k = w.shape[-1]
+    pad = dilation * (k - 1) // 2 if padding is None else padding
+    return [w[:, :, j] for j in range(k)], [j * dilation - pad for j in range(k)]
+
+
+def convtr_phases(w: torch.Tensor, u: int, padding: int):
+    """ConvTranspose1d weight [ci, co, K], stride u -> per output phase rho (s = u*q + rho):
+    (tap matrices [co, ci], input offsets) with y[u*q + rho] = sum_m W_m x[q + off_m]."""
+    K = w.shape[-1]
+    assert K % u == 0, "kernel must be a multiple of the stride"
+    phases = []
+    for rho in range(u):
+        r = (rho + padding) % u
+        base = (rho + padding) // u
+        taps = [w[:, :, r + u * m].t().contiguous() for m in range(K // u)]
+        offs = [base - m for m in range(K // u)]
+        phases.append((taps, offs))
+    return phases
+
+
+class _Conv:
+    def __init__(self, taps, offs, bias, cin, cout, device):
+        self.w = pack_taps(taps, cin, cout).to(device)
+        self.offs = _hip.i32_array(offs)
+        self.ntaps = len(offs)
+        self.bias = bias.float().to(device) if bias is not None else None
+        self.cin, self.cout = cin, cout
+
+
+class _Act:
+    def __init__(self, sd, prefix, device):
+        self.up = sd[prefix + ".upsample.filter"].reshape(-1).float().to(device)
+        self.down = sd[prefix + ".downsample.lowpass.filter"].reshape(-1).float().to(device)
+        self.alpha = sd[prefix + ".act.alpha"].float().to(device)
+        self.beta = sd[prefix + ".act.beta"].float().to(device)
+        assert self.up.numel() == 12 and self.down.numel() == 12, "kernel implements the 12-tap Activation1d"
+
+
+class HipBigVGAN:
+    def __init__(self, state_dict, cfg_bv, device="cuda"):
+        self.lib = _hip.load()
+        self.h = h = cfg_bv
+        self.device = torch.device(device)
+        sd = fold_weight_norm(state_dict)
+        self.sd_torch = {k: v.to(self.device) for k, v in sd.items() if k.startswith(("speaker_encoder", "cond_layer", "conds"))}
+        dev = self.device
+        w = sd["conv_pre.weight"]
+        taps, offs = conv1d_taps(w)
+        self.conv_pre = _Conv(taps, offs, sd["conv_pre.bias"], w.shape[1], w.shape[0], dev)
+        self.ups = []
+        for i, (u, k) in enumerate(zip(h.upsample_rates, h.upsample_kernel_sizes)):
+            wt = sd[f"ups.{i}.0.weight"]
+            u, k = int(u), int(k)
+            phases = [(_Conv(t, o, sd[f"ups.{i}.0.bias"], wt.shape[0], wt.shape[1], dev)) for t, o in
+                      convtr_phases(wt, u, (k - u) // 2)]
+            self.ups.append((u, phases))
+        self.nk = len(h.resblock_kernel_sizes)
+        self.blocks = []
+        for i in range(len(h.upsample_rates)):
+            stage = []
+            for j, (k, dils) in enumerate(zip(h.resblock_kernel_sizes, h.resblock_dilation_sizes)):
+                p = f"resblocks.{i * self.nk + j}"
+                layers = []
+                for n, d in enumerate(dils):
+                    w1 = sd[f"{p}.convs1.{n}.weight"]
+                    w2 = sd[f"{p}.convs2.{n}.weight"]
+                    c1 = _Conv(*conv1d_taps(w1, int(d)), sd[f"{p}.convs1.{n}.bias"], w1.shape[1], w1.shape[0], dev)
+                    c2 = _Conv(*conv1d_taps(w2, 1), sd[f"{p}.convs2.{n}.bias"], w2.shape[1], w2.shape[0], dev)
+                    layers.append((_Act(sd, f"{p}.activations.{2 * n}", dev), c1,
+                                   _Act(sd, f"{p}.activations.{2 * n + 1}", dev), c2))
+                stage.append(layers)
+            self.blocks.append(stage)
+        self.act_post = _Act(sd, "activation_post", dev)
+        wp = sd["conv_post.weight"]  # [1, C, K]
+        self.post_w = wp[0].contiguous().float().to(dev)
+        self.post_b = float(sd["conv_post.bias"].reshape(-1)[0])
+        self.post_k = wp.shape[-1]
+        self.hop = int(np.prod([int(u) for u in h.upsample_rates]))
+        self._bufs = {}
+
+    # ---------------- per-prompt (cached by the caller) ----------------
+    @torch.no_grad()
+    def speaker(self, mel_ref: torch.Tensor) -> torch.Tensor:
+        """mel_ref [B, T, n_mels] -> [B, spk_dim] (ECAPA; PyTorch ops on the device)."""
+        return speaker_embedding(self.sd_torch, mel_ref.to(self.device).float())
+
+    @torch.no_grad()
+    def cond_biases(self, spk: torch.Tensor):
+        s = spk.float()
+        pre = F.linear(s, self.sd_torch["cond_layer.weight"][:, :, 0], self.sd_torch["cond_layer.bias"])
+        per = [F.linear(s, self.sd_torch[f"conds.{i}.weight"][:, :, 0], self.sd_torch[f"conds.{i}.bias"])
+               for i in range(len(self.ups))]
+        return pre.contiguous(), [p.contiguous() for p in per]
+
+    # ---------------- launches ----------------
+    def _buf(self, name, shape, dtype=torch.bfloat16):
+        key = (name, dtype)
+        b = self._bufs.get(key)
+        n = int(np.prod(shape))
+        if b is None or b.numel() < n:
+            b = torch.empty(n, dtype=dtype, device=self.device)
+            self._bufs[key] = b
+        return b[:n].view(*shape)
+
+    def _act(self, a: _Act, x, y, lens):
+        B, T, C = x.shape
+        _hip.check(self.lib.itts_aa_snakebeta_fwd(
+            x.data_ptr(), y.data_ptr(), a.up.data_ptr(), a.down.data_ptr(), a.alpha.data_ptr(), a.beta.data_ptr(),
+            lens.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1, _hip.dtype_code(x), _hip.dtype_code(y),
+            _hip.stream_ptr()), "itts_aa_snakebeta_fwd")
+
+    def _conv(self, c: _Conv, x, y, lens, r1=None, r2=None, alpha=1.0, bias_b=None, ymul=1, yoff=0, Tq=None):
+        B, T, Cin = x.shape
+        Ty = y.shape[1]
+        _hip.check(self.lib.itts_igemm_fwd(
+            x.data_ptr(), T * Cin, Cin, c.w.data_ptr(), _hip.ptr(c.bias), _hip.ptr(bias_b), _hip.ptr(r1),
+            _hip.ptr(r2), y.data_ptr(), Ty * y.shape[2], y.shape[2], lens.data_ptr(), B, T if Tq is None else Tq,
+            Cin, c.cout, c.ntaps, c.offs, ymul, yoff, float(alpha), 0, _hip.dtype_code(y), _hip.stream_ptr()),
+            "itts_igemm_fwd")
+
+    @torch.no_grad()
+    def forward(self, latent: torch.Tensor, lengths: torch.Tensor, spk: torch.Tensor, want_pcm: bool = True):
+        """latent [B, T, gpt_dim] (bf16/f32, device), lengths [B] frames, spk [B, spk_dim]
+        -> (wav f32 [B, T*hop], pcm int16 [B, T*hop] or None); samples past lengths*hop are undefined."""
+        dev = self.device
+        x = latent.to(dev)
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        x = x.contiguous()
+        B, T, _ = x.shape
+        lens = lengths.to(dev, torch.int32).contiguous()
+        pre_b, stage_b = self.cond_biases(spk.to(dev))
+        C0 = self.conv_pre.cout
+        cur_in = self._buf("xs_a", (B, T, C0))
+        self._conv(self.conv_pre, x, cur_in, lens, bias_b=pre_b)
+        Tcur = T
+        for i, (u, phases) in enumerate(self.ups):
+            C = phases[0].cout
+            Tn = Tcur * u
+            lens_n = (lens * u).contiguous()
+            x_st = self._buf("x", (B, Tn, C))
+            for rho, ph in enumerate(phases):
+                self._conv(ph, cur_in, x_st, lens, bias_b=stage_b[i], ymul=u, yoff=rho)
+            t1 = self._buf("t1", (B, Tn, C))
+            t2 = self._buf("t2", (B, Tn, C))
+            cur = self._buf("cur", (B, Tn, C))
+            xs = self._buf("xs_b" if i % 2 == 0 else "xs_a", (B, Tn, C))
+            for j, layers in enumerate(self.blocks[i]):
+                src = x_st
+                for n, (a1, c1, a2, c2) in enumerate(layers):
+                    self._act(a1, src, t1, lens_n)
+                    self._conv(c1, t1, t2, lens_n)
+                    self._act(a2, t2, t1, lens_n)
+                    if n < len(layers) - 1:
+                        self._conv(c2, t1, cur, lens_n, r1=src)
+                        src = cur
+                    else:
+                        last = j == self.nk - 1
+                        self._conv(c2, t1, xs, lens_n, r1=src, r2=xs if j > 0 else None,
+                                   alpha=(1.0 / self.nk) if last else 1.0)
+            cur_in, Tcur, lens = xs, Tn, lens_n
+        t1 = self._buf("t1", cur_in.shape)
+        self._act(self.act_post, cur_in, t1, lens)
+        wav = torch.empty(B, Tcur, dtype=torch.float32, device=dev)
+        pcm = torch.empty(B, Tcur, dtype=torch.int16, device=dev) if want_pcm else None
+        C = t1.shape[2]
+        _hip.check(self.lib.itts_conv_post_tanh(
+            t1.data_ptr(), Tcur * C, C, self.post_w.data_ptr(), self.post_b, C, self.post_k, lens.data_ptr(), B, Tcur,
+            wav.data_ptr(), _hip.ptr(pcm), Tcur, _hip.dtype_code(t1), _hip.stream_ptr()), "itts_conv_post_tanh")
+        return wav, pcm

@@ -1,0 +1,136 @@
+"""GPU parity of the BigVGAN2 HIP path (through the C ABI) against the CPU oracle / reference goldens.
+
+Tolerances (stated per the north star: vocoder within fp tolerance):
+  * Activation1d kernel, f32 in/out: max |err| <= 5e-5 (f32 math; accurate sinf)
+  * implicit-GEMM conv, bf16 in / f32 out: max |err| <= 1e-4 * sum|w||x| (f32 accumulation of the
+    same bf16-rounded operands)
+  * full vocoder in bf16 storage vs the fp32 oracle: waveform relative RMS error <= 2e-2 and
+    max |err| <= 0.05; int16 output max |diff| <= 0.05 * 32767
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from indextts import _hip
+    return _hip, _hip.load()
+
+
+@pytest.mark.parametrize("i", range(5))
+def test_activation_kernel_bct_matches_golden(golden, i):
+    _hip, lib = _lib()
+    x = torch.from_numpy(golden[f"act{i}_x"]).cuda()
+    f = torch.from_numpy(golden[f"act{i}_filter"]).reshape(-1).cuda()
+    a = torch.from_numpy(golden[f"act{i}_alpha"]).cuda()
+    b = torch.from_numpy(golden[f"act{i}_beta"]).cuda()
+    y = torch.empty_like(x)
+    B, C, T = x.shape
+    _hip.check(lib.itts_aa_snakebeta_bct(x.data_ptr(), y.data_ptr(), f.data_ptr(), f.data_ptr(), a.data_ptr(),
+                                         b.data_ptr(), B, C, T, _hip.F32, _hip.stream_ptr()), "bct")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(y.cpu().numpy(), golden[f"act{i}_y"], rtol=0, atol=5e-5)
+
+
+def test_activation_kernel_ragged_channel_last():
+    from oracle.bigvgan_oracle import activation1d
+    from indextts.utils.synthetic import kaiser_sinc_lowpass
+    _hip, lib = _lib()
+    torch.manual_seed(0)
+    B, T, C = 3, 301, 40
+    lens = torch.tensor([301, 17, 2], dtype=torch.int32)
+    x = torch.randn(B, T, C)
+    f = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1)
+    la, lb = torch.randn(C) * 0.5, torch.randn(C) * 0.5
+    xd, y = x.cuda(), torch.zeros(B, T, C, device="cuda")
+    fd, lad, lbd, lensd = f.cuda(), la.cuda(), lb.cuda(), lens.cuda()
+    _hip.check(lib.itts_aa_snakebeta_fwd(xd.data_ptr(), y.data_ptr(), fd.data_ptr(), fd.data_ptr(), lad.data_ptr(),
+                                         lbd.data_ptr(), lensd.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1,
+                                         _hip.F32, _hip.F32, _hip.stream_ptr()), "fwd")
+    torch.cuda.synchronize()
+    yc = y.cpu()
+    for b in range(B):
+        L = int(lens[b])
+        ref = activation1d(x[b:b + 1, :L].transpose(1, 2), f, f, la, lb)[0].t()
+        np.testing.assert_allclose(yc[b, :L].numpy(), ref.numpy(), rtol=0, atol=5e-5)
+
+
+@pytest.mark.parametrize("cin,cout,k,d", [(768, 768, 3, 5), (96, 96, 11, 3), (24, 24, 7, 1), (1024, 1536, 7, 1),
+                                          (12, 6, 3, 1), (40, 200, 5, 2)])
+def test_igemm_conv_matches_torch(cin, cout, k, d):
+    from indextts.vocoder.bigvgan import _Conv, conv1d_taps
+    _hip, lib = _lib()
+    torch.manual_seed(cin + cout)
+    B, T = 2, 150
+    lens = torch.tensor([150, 61], dtype=torch.int32)
+    x = torch.randn(B, T, cin).to(torch.bfloat16)
+    w = torch.randn(cout, cin, k) / (cin * k) ** 0.5
+    bias = torch.randn(cout) * 0.1
+    conv = _Conv(*conv1d_taps(w, d), bias, cin, cout, "cuda")
+    y = torch.zeros(B, T, cout, device="cuda")
+    xd, lensd = x.cuda(), lens.cuda()
+    _hip.check(lib.itts_igemm_fwd(xd.data_ptr(), T * cin, cin, conv.w.data_ptr(), conv.bias.data_ptr(), None, None,
+                                  None, y.data_ptr(), T * cout, cout, lensd.data_ptr(), B, T, cin, cout, conv.ntaps,
+                                  conv.offs, 1, 0, 1.0, 0, _hip.F32, _hip.stream_ptr()), "igemm")
+    torch.cuda.synchronize()
+    wq = w.to(torch.bfloat16).float()
+    for b in range(B):
+        L = int(lens[b])
+        ref = F.conv1d(x[b:b + 1, :L].float().transpose(1, 2), wq, bias, dilation=d, padding=d * (k - 1) // 2)[0].t()
+        scale = F.conv1d(x[b:b + 1, :L].float().abs().transpose(1, 2), wq.abs(), dilation=d,
+                         padding=d * (k - 1) // 2)[0].t()
+        err = (y[b, :L].cpu() - ref).abs()
+        assert bool((err <= 1e-4 * scale + 1e-5).all()), float(err.max())
+
+
+def _vocoder(tag):
+    from indextts.utils.config import load_config, default_config_path, tiny_config
+    from indextts.utils.synthetic import bigvgan_state_dict
+    from indextts.vocoder.bigvgan import HipBigVGAN
+    from oracle.bigvgan_oracle import BigVGANOracle
+    cfg = tiny_config() if tag == "tiny" else load_config(default_config_path())
+    sd = bigvgan_state_dict(cfg.bigvgan, 0)
+    return HipBigVGAN(sd, cfg.bigvgan, "cuda"), BigVGANOracle(sd, cfg.bigvgan)
+
+
+@pytest.mark.parametrize("tag", ["tiny", "full"])
+def test_vocoder_matches_reference_golden(golden, tag):
+    voc, _ = _vocoder(tag)
+    lat = torch.from_numpy(golden[f"{tag}_bv_latent"]).cuda()
+    spk = torch.from_numpy(golden[f"{tag}_bv_spk"]).cuda()
+    wav, pcm = voc.forward(lat, torch.tensor([lat.shape[1]]), spk)
+    torch.cuda.synchronize()
+    ref = golden[f"{tag}_bv_wav"][:, 0]
+    got = wav.cpu().numpy()
+    rel = np.sqrt(np.mean((got - ref) ** 2) / np.mean(ref ** 2))
+    assert rel <= 2e-2, rel
+    assert np.abs(got - ref).max() <= 0.05
+    d = np.abs(pcm.cpu().numpy().astype(np.int32) - golden[f"{tag}_bv_int16"][:, 0].astype(np.int32))
+    assert d.max() <= 0.05 * 32767
+
+
+def test_vocoder_speaker_embedding_on_device(golden):
+    voc, _ = _vocoder("tiny")
+    spk = voc.speaker(torch.from_numpy(golden["tiny_bv_mel_ref"]).cuda())
+    np.testing.assert_allclose(spk.cpu().numpy(), golden["tiny_bv_spk"], rtol=1e-3, atol=1e-3)
+
+
+def test_vocoder_ragged_batch_equals_single():
+    """Utterances of different lengths in one batch produce what each produces alone (bit-exact)."""
+    voc, orc = _vocoder("tiny")
+    torch.manual_seed(3)
+    T = 11
+    lat = torch.randn(3, T, 256)
+    spk = torch.randn(3, 512)
+    lens = torch.tensor([11, 6, 1])
+    wav, _ = voc.forward(lat.cuda(), lens, spk.cuda(), want_pcm=False)
+    for b in range(3):
+        L = int(lens[b])
+        w1, _ = voc.forward(lat[b:b + 1, :L].cuda(), torch.tensor([L]), spk[b:b + 1].cuda(), want_pcm=False)
+        torch.testing.assert_close(wav[b, :L * 1024].cpu(), w1[0].cpu(), rtol=0, atol=0)
+        ref = orc.forward(lat[b:b + 1, :L], spk[b:b + 1])[0, 0]
+        rel = float(((w1[0].cpu() - ref) ** 2).mean().sqrt() / (ref ** 2).mean().sqrt())
+        assert rel <= 2e-2, rel
