@@ -1,0 +1,258 @@
+// GPT-2 self-attention (16 heads x 64, scale 1/8, causal + left-padding key mask) for gfx950.
+// Math: HF:modeling_gpt2.py:54-72 (softmax(q k^T * 1/sqrt(64) + mask) v, f32); padding semantics
+// of prepare_gpt_inputs (gpt/model.py:628-635: keys of left-pad positions masked, quirk Q2).
+//
+// 1. itts_attn_decode: one new token per sequence.  Appends its k/v (from the QKV projection, f32)
+//    into the KV cache at index kv_base + *t (device counter -> hipGraph-replayable), then attends
+//    over keys [pad_b, kv_base + *t].  One 256-thread workgroup per (head, sequence); scores use
+//    8 lanes per key (one 1 KiB coalesced wave load = 8 key rows), softmax via workgroup reductions,
+//    P.V with 8 lanes per key-row slice reduced through LDS.
+// 2. itts_attn_prefill: variable-length causal attention over packed sequences (prefill of the
+//    prompt block, and the teacher-forced latent pass).  One thread per query, K/V staged through
+//    LDS in 32-key blocks, block-wise online softmax; optionally writes K/V into the decode cache.
+#include "common.h"
+
+namespace {
+
+constexpr int kHD = 64;
+
+template <typename TC>
+__device__ __forceinline__ void load8(const TC* p, float (&v)[8]);
+template <>
+__device__ __forceinline__ void load8<float>(const float* p, float (&v)[8]) {
+  const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p), b = *reinterpret_cast<const f32x4_t*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+template <>
+__device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]) {
+  const u32x4_t a = *reinterpret_cast<const u32x4_t*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(a[i] << 16);
+    v[2 * i + 1] = __uint_as_float(a[i] & 0xFFFF0000u);
+  }
+}
+
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+  return r;
+}
+
+constexpr int kMaxKeys = 2048;
+
+template <typename TC, typename TO>
+__global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv,
+                                                          TC* __restrict__ cache_k, TC* __restrict__ cache_v,
+                                                          int64_t cache_bs, int64_t cache_hs, const int32_t* pad,
+                                                          int kv_base, const int32_t* __restrict__ tstate,
+                                                          TO* __restrict__ out, int64_t ldo, int H) {
+  __shared__ float qs[kHD], kn[kHD], vn[kHD];
+  __shared__ float sc[kMaxKeys];
+  __shared__ float red[8];
+  __shared__ float pv[32][kHD + 1];
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int D = H * kHD;
+  const int kidx = kv_base + tstate[0];
+  const int p0 = pad ? pad[b] : 0;
+  const int nk = kidx + 1 - p0;
+  const float* row = qkv + (int64_t)b * ldqkv + h * kHD;
+  TC* Kc = cache_k + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
+  TC* Vc = cache_v + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
+  if (threadIdx.x < kHD) {
+    const int d = threadIdx.x;
+    qs[d] = row[d];
+    const float k = row[D + d], v = row[2 * D + d];
+    kn[d] = k;
+    vn[d] = v;
+    St<TC>::st(Kc + (int64_t)kidx * kHD + d, k);
+    St<TC>::st(Vc + (int64_t)kidx * kHD + d, v);
+  }
+  __syncthreads();
+  const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
+  float q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = qs[8 * d8 + e];
+  // scores for keys p0 .. kidx (the new key from LDS so the just-written cache line is never re-read)
+  float lmax = -INFINITY;
+  for (int j0 = 0; j0 < nk; j0 += 32) {
+    const int j = j0 + g;
+    float part = 0.f;
+    if (j < nk) {
+      float k[8];
+      if (p0 + j == kidx) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) k[e] = kn[8 * d8 + e];
+      } else {
+        load8<TC>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8, k);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part = fmaf(q[e], k[e], part);
+    }
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64);
+    if (j < nk && d8 == 0) {
+      const float s = part * 0.125f;
+      sc[j] = s;
+      lmax = fmaxf(lmax, s);
+    }
+  }
+  const float mx = block_reduce(lmax, red, true);
+  float lsum = 0.f;
+  for (int j = threadIdx.x; j < nk; j += 256) {
+    const float e = __expf(sc[j] - mx);
+    sc[j] = e;
+    lsum += e;
+  }
+  const float inv = 1.0f / block_reduce(lsum, red, false);  // includes a barrier: sc[] complete
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j = g; j < nk; j += 32) {
+    float v[8];
+    if (p0 + j == kidx) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = vn[8 * d8 + e];
+    } else {
+      load8<TC>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8, v);
+    }
+    const float p = sc[j];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = fmaf(p, v[e], o[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pv[g][8 * d8 + e] = o[e];
+  __syncthreads();
+  if (threadIdx.x < kHD) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) s += pv[i][threadIdx.x];
+    St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, s * inv);
+  }
+}
+
+constexpr int kQB = 128;  // queries per workgroup (one per thread)
+constexpr int kKB = 32;   // keys per LDS block
+
+template <typename TC, typename TO>
+__global__ __launch_bounds__(kQB) void attn_prefill_kernel(const float* __restrict__ qkv, int64_t ldqkv,
+                                                           const int32_t* __restrict__ seq_start,
+                                                           const int32_t* __restrict__ seq_len,
+                                                           const int32_t* __restrict__ seq_pad, TC* cache_k,
+                                                           TC* cache_v, int64_t cache_bs, int64_t cache_hs,
+                                                           TO* __restrict__ out, int64_t ldo, int H) {
+  __shared__ float Ks[kKB][kHD], Vs[kKB][kHD];
+  const int qb = blockIdx.x, h = blockIdx.y, sq = blockIdx.z;
+  const int len = seq_len[sq], p0 = seq_pad ? seq_pad[sq] : 0;
+  const int q_lo = qb * kQB;
+  if (q_lo >= len) return;
+  const int q_hi = min(q_lo + kQB, len);
+  const int D = H * kHD;
+  const float* base = qkv + (int64_t)seq_start[sq] * ldqkv;
+  const int i = q_lo + threadIdx.x;
+  const bool active = i < len && i >= p0;
+  float q[kHD], o[kHD];
+#pragma unroll
+  for (int d = 0; d < kHD; ++d) {
+    q[d] = active ? base[(int64_t)i * ldqkv + h * kHD + d] * 0.125f : 0.f;
+    o[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int kb = p0; kb < q_hi; kb += kKB) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < kKB * kHD; e += kQB) {
+      const int r = e / kHD, d = e % kHD, j = kb + r;
+      float kv = 0.f, vv = 0.f;
+      if (j < len) {
+        kv = base[(int64_t)j * ldqkv + D + h * kHD + d];
+        vv = base[(int64_t)j * ldqkv + 2 * D + h * kHD + d];
+        if (cache_k && j >= q_lo && j < q_hi) {
+          St<TC>::st(cache_k + (int64_t)sq * cache_bs + (int64_t)h * cache_hs + (int64_t)j * kHD + d, kv);
+          St<TC>::st(cache_v + (int64_t)sq * cache_bs + (int64_t)h * cache_hs + (int64_t)j * kHD + d, vv);
+        }
+      }
+      Ks[r][d] = kv;
+      Vs[r][d] = vv;
+    }
+    __syncthreads();
+    if (!active || kb > i) continue;
+    const int nvalid = min(kKB, i - kb + 1);
+    float s[kKB];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < kKB; ++r) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < kHD; ++d) acc = fmaf(q[d], Ks[r][d], acc);
+      s[r] = r < nvalid ? acc : -INFINITY;
+      bm = fmaxf(bm, s[r]);
+    }
+    const float mn = fmaxf(m, bm);
+    const float corr = __expf(m - mn);
+    l *= corr;
+#pragma unroll
+    for (int d = 0; d < kHD; ++d) o[d] *= corr;
+#pragma unroll
+    for (int r = 0; r < kKB; ++r) {
+      const float p = __expf(s[r] - mn);
+      l += p;
+#pragma unroll
+      for (int d = 0; d < kHD; ++d) o[d] = fmaf(p, Vs[r][d], o[d]);
+    }
+    m = mn;
+  }
+  if (i < len) {
+    TO* orow = out + (int64_t)(seq_start[sq] + i) * ldo + h * kHD;
+    const float inv = active ? 1.0f / l : 0.f;
+#pragma unroll
+    for (int d = 0; d < kHD; ++d) St<TO>::st(orow + d, o[d] * inv);
+  }
+}
+
+}  // namespace
+
+extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, void* cache_k, void* cache_v, int64_t cache_bs,
+                                int64_t cache_hs, int smax, const int32_t* pad, int kv_base, const int32_t* tstate,
+                                void* out, int64_t ldo, int B, int H, int cache_dtype, int out_dtype, void* stream) {
+  const char* fn = "itts_attn_decode";
+  ITTS_REQUIRE(B >= 0 && H > 0, fn, "bad sizes");
+  if (B == 0) return 0;
+  ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && out, fn, "null pointer");
+  ITTS_REQUIRE(smax <= kMaxKeys && cache_hs >= (int64_t)smax * kHD, fn, "cache capacity exceeds 2048 keys");
+  dim3 grid(H, B);
+  hipStream_t s = itts::as_stream(stream);
+#define ITTS_AD(TC, TO)                                                                                          \
+  hipLaunchKernelGGL((attn_decode_kernel<TC, TO>), grid, dim3(256), 0, s, qkv, ldqkv, (TC*)cache_k, (TC*)cache_v, \
+                     cache_bs, cache_hs, pad, kv_base, tstate, (TO*)out, ldo, H)
+  if (cache_dtype == ITTS_BF16 && out_dtype == ITTS_BF16) ITTS_AD(uint16_t, uint16_t);
+  else if (cache_dtype == ITTS_F32 && out_dtype == ITTS_F32) ITTS_AD(float, float);
+  else if (cache_dtype == ITTS_BF16) ITTS_AD(uint16_t, float);
+  else ITTS_AD(float, uint16_t);
+#undef ITTS_AD
+  return itts::check_launch(fn);
+}
+
+extern "C" int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start, const int32_t* seq_len,
+                                 const int32_t* seq_pad, int nseq, int max_len, void* cache_k, void* cache_v,
+                                 int64_t cache_bs, int64_t cache_hs, void* out, int64_t ldo, int H, int cache_dtype,
+                                 int out_dtype, void* stream) {
+  const char* fn = "itts_attn_prefill";
+  ITTS_REQUIRE(nseq >= 0 && H > 0 && max_len >= 0, fn, "bad sizes");
+  if (nseq == 0 || max_len == 0) return 0;
+  ITTS_REQUIRE(qkv && seq_start && seq_len && out, fn, "null pointer");
+  dim3 grid((max_len + kQB - 1) / kQB, H, nseq);
+  hipStream_t s = itts::as_stream(stream);
+#define ITTS_AP(TC, TO)                                                                                           \
+  hipLaunchKernelGGL((attn_prefill_kernel<TC, TO>), grid, dim3(kQB), 0, s, qkv, ldqkv, seq_start, seq_len, seq_pad, \
+                     (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, (TO*)out, ldo, H)
+  if (cache_dtype == ITTS_BF16 && out_dtype == ITTS_BF16) ITTS_AP(uint16_t, uint16_t);
+  else if (cache_dtype == ITTS_F32 && out_dtype == ITTS_F32) ITTS_AP(float, float);
+  else if (cache_dtype == ITTS_BF16) ITTS_AP(uint16_t, float);
+  else ITTS_AP(float, uint16_t);
+#undef ITTS_AP
+  return itts::check_launch(fn);
+}

@@ -1,0 +1,139 @@
+// LayerNorm family for the GPT-2 core (HF GPT2Block ln_1/ln_2, ln_f, then UnifiedVoice.final_norm;
+// eps 1e-5, HF:modeling_gpt2.py:246-306,620; gpt/model.py:48 -- quirk Q5 double LN before mel_head).
+//
+//  * itts_layernorm_rows: y[m] = LN2?(LN1(x[m])) for M rows of width D (x f32, y f32|bf16),
+//    optional row gather (y row m <- x row idx[m]) so the prefill can normalise only each
+//    sequence's last position.
+//  * itts_residual_reduce_ln: decode-step split-K epilogue
+//       x[b] += bias + sum_s part[s][b]          (deterministic fixed-order sum, no atomics)
+//       h[b]  = LN2?(LN1(x[b]))                 (input of the next projection GEMM)
+// One 256-thread workgroup per row; two-pass (mean, then centred variance) in f32 like torch.
+#include "common.h"
+
+namespace {
+constexpr int kT = 256;
+constexpr int kMaxPer = 16;  // D <= 4096
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kT / 64; ++i) s += red[i];
+  return s;
+}
+
+// normalise the per-thread slice v[0..n) (element index = threadIdx.x + kT*i) in place
+__device__ __forceinline__ void ln_inplace(float (&v)[kMaxPer], int n, int D, const float* g, const float* b,
+                                           float* red) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxPer; ++i)
+    if (i < n) s += v[i];
+  const float mean = block_sum(s, red) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxPer; ++i)
+    if (i < n) {
+      float d = v[i] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(block_sum(q, red) / D + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < kMaxPer; ++i)
+    if (i < n) {
+      int e = threadIdx.x + kT * i;
+      v[i] = (v[i] - mean) * rstd * g[e] + b[e];
+    }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(kT) void ln_rows_kernel(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ idx,
+                                                     TO* __restrict__ y, int64_t ldy, int D, const float* g1,
+                                                     const float* b1, const float* g2, const float* b2) {
+  __shared__ float red[kT / 64];
+  const int m = blockIdx.x;
+  const float* xr = x + (int64_t)(idx ? idx[m] : m) * ldx;
+  float v[kMaxPer];
+  const int n = (D - threadIdx.x + kT - 1) / kT;
+#pragma unroll
+  for (int i = 0; i < kMaxPer; ++i)
+    if (i < n) v[i] = xr[threadIdx.x + kT * i];
+  ln_inplace(v, n, D, g1, b1, red);
+  if (g2) ln_inplace(v, n, D, g2, b2, red);
+  TO* yr = y + (int64_t)m * ldy;
+#pragma unroll
+  for (int i = 0; i < kMaxPer; ++i)
+    if (i < n) St<TO>::st(yr + threadIdx.x + kT * i, v[i]);
+}
+
+template <typename TO>
+__global__ __launch_bounds__(kT) void residual_reduce_ln_kernel(float* __restrict__ x, int64_t ldx,
+                                                                const float* __restrict__ part, int nsplit,
+                                                                int64_t split_stride, int64_t ldp,
+                                                                const float* __restrict__ bias, TO* __restrict__ h,
+                                                                int64_t ldh, int D, const float* g1, const float* b1,
+                                                                const float* g2, const float* b2) {
+  __shared__ float red[kT / 64];
+  const int m = blockIdx.x;
+  float* xr = x + (int64_t)m * ldx;
+  float v[kMaxPer];
+  const int n = (D - threadIdx.x + kT - 1) / kT;
+#pragma unroll
+  for (int i = 0; i < kMaxPer; ++i) {
+    if (i < n) {
+      const int e = threadIdx.x + kT * i;
+      float acc = bias ? bias[e] : 0.f;
+      for (int s = 0; s < nsplit; ++s) acc += part[s * split_stride + (int64_t)m * ldp + e];
+      v[i] = xr[e] + acc;
+      xr[e] = v[i];
+    }
+  }
+  if (g1) {
+    ln_inplace(v, n, D, g1, b1, red);
+    if (g2) ln_inplace(v, n, D, g2, b2, red);
+    TO* hr = h + (int64_t)m * ldh;
+#pragma unroll
+    for (int i = 0; i < kMaxPer; ++i)
+      if (i < n) St<TO>::st(hr + threadIdx.x + kT * i, v[i]);
+  }
+}
+}  // namespace
+
+extern "C" int itts_layernorm_rows(const float* x, int64_t ldx, const int32_t* row_idx, void* y, int64_t ldy, int M,
+                                   int D, const float* g1, const float* b1, const float* g2, const float* b2,
+                                   int out_dtype, void* stream) {
+  const char* fn = "itts_layernorm_rows";
+  ITTS_REQUIRE(M >= 0 && D > 0 && D <= kT * kMaxPer, fn, "D must be in [1, 4096]");
+  if (M == 0) return 0;
+  ITTS_REQUIRE(x && y && g1 && b1 && (!g2 || b2), fn, "null pointer");
+  hipStream_t s = itts::as_stream(stream);
+  if (out_dtype == ITTS_BF16)
+    hipLaunchKernelGGL(ln_rows_kernel<uint16_t>, dim3(M), dim3(kT), 0, s, x, ldx, row_idx, (uint16_t*)y, ldy, D, g1,
+                       b1, g2, b2);
+  else
+    hipLaunchKernelGGL(ln_rows_kernel<float>, dim3(M), dim3(kT), 0, s, x, ldx, row_idx, (float*)y, ldy, D, g1, b1, g2,
+                       b2);
+  return itts::check_launch(fn);
+}
+
+extern "C" int itts_residual_reduce_ln(float* x, int64_t ldx, const float* part, int nsplit, int64_t split_stride,
+                                       int64_t ldp, const float* bias, void* h, int64_t ldh, int M, int D,
+                                       const float* g1, const float* b1, const float* g2, const float* b2,
+                                       int out_dtype, void* stream) {
+  const char* fn = "itts_residual_reduce_ln";
+  ITTS_REQUIRE(M >= 0 && D > 0 && D <= kT * kMaxPer && nsplit >= 0, fn, "bad sizes");
+  if (M == 0) return 0;
+  ITTS_REQUIRE(x && (nsplit == 0 || part) && (!g1 || (b1 && h)), fn, "null pointer");
+  hipStream_t s = itts::as_stream(stream);
+  if (out_dtype == ITTS_BF16)
+    hipLaunchKernelGGL(residual_reduce_ln_kernel<uint16_t>, dim3(M), dim3(kT), 0, s, x, ldx, part, nsplit,
+                       split_stride, ldp, bias, (uint16_t*)h, ldh, D, g1, b1, g2, b2);
+  else
+    hipLaunchKernelGGL(residual_reduce_ln_kernel<float>, dim3(M), dim3(kT), 0, s, x, ldx, part, nsplit, split_stride,
+                       ldp, bias, (float*)h, ldh, D, g1, b1, g2, b2);
+  return itts::check_launch(fn);
+}

@@ -39,6 +39,19 @@ SIGNATURES = {
                               _c_i, _c_i, _c_i, _i32p, _c_i, _c_i, _c_f, _c_i, _c_i, _vp]),
     "itts_conv_post_tanh": (_c_i, [_vp, _c_i64, _c_i64, _vp, _c_f, _c_i, _c_i, _vp, _c_i, _c_i, _vp, _vp, _c_i64,
                                    _c_i, _vp]),
+    "itts_layernorm_rows": (_c_i, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp, _vp, _vp, _c_i, _vp]),
+    "itts_residual_reduce_ln": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp,
+                                       _vp, _vp, _c_i, _vp]),
+    "itts_skinny_gemm_bf16": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _c_i, _vp, _c_i64, _c_i, _vp, _c_i64,
+                                     _c_i, _vp]),
+    "itts_gemm_f32": (_c_i, [_vp, _c_i64, _vp, _c_i64, _c_i, _c_i, _c_i, _vp, _c_i, _vp, _vp, _c_i64, _vp]),
+    "itts_attn_decode": (_c_i, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_i, _vp, _c_i, _vp, _vp, _c_i64, _c_i, _c_i,
+                                _c_i, _c_i, _vp]),
+    "itts_attn_prefill": (_c_i, [_vp, _c_i64, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i,
+                                 _c_i, _c_i, _vp]),
+    "itts_sample_embed": (_c_i, [_vp, _c_i64, _c_i, _vp, _vp, _vp, _c_i64, _vp, _c_i, _c_i, _c_i, _c_f, _vp, _vp, _c_i,
+                                 _c_i, _vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp]),
+    "itts_step_advance": (_c_i, [_vp, _c_i, _vp]),
 }
 
 _lib = None

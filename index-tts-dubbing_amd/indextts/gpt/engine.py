@@ -1,0 +1,404 @@
+"""UnifiedVoice speech-token GPT on the HIP C-ABI: prefill, KV-cached greedy decode, latent pass.
+
+Host mirror of ``UnifiedVoice.inference_speech`` (reference ``indextts/gpt/model.py:655-708``) and
+``UnifiedVoice.forward(..., return_latent=True)`` (``:521-589``) for a batch of utterances.
+
+Two numeric modes:
+  * ``bf16`` (product): bf16 weights, bf16 GEMM operands with f32 accumulation (MFMA), f32
+    residual stream / LayerNorm / softmax / logits, bf16 KV cache.
+  * ``f32`` (verification): f32 weights/activations/cache through exact-f32 VALU GEMMs; used to
+    show bit-exact greedy ids against the fp32 reference.
+
+HBM layout (per engine, batch capacity B): residual x [B, D] f32; GEMM operands padded to 32-row
+MFMA tiles; KV cache [layers][B][heads][Smax][64]; decode state (token counter, seen-id bitmap,
+done flags, codes) lives on the device so one captured hipGraph replays every step.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .. import _hip
+from .conditioning import get_conditioning
+
+
+def _t(v):
+    return v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+
+
+def pack_skinny(w_t: torch.Tensor) -> torch.Tensor:
+    """W^T [N, K] f32 -> MFMA-fragment order [N/32][K/16][64 lanes][8] bf16 (lane = 32*h + r holds
+    W^T[32*nt + r][16*s + 8*h : +8]); N zero-padded to a multiple of 32."""
+    N, K = w_t.shape
+    assert K % 16 == 0
+    Np = (N + 31) // 32 * 32
+    w = torch.zeros(Np, K, dtype=torch.float32)
+    w[:N] = w_t.float()
+    w = w.reshape(Np // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
+    return w.to(torch.bfloat16)
+
+
+class _Layer:
+    pass
+
+
+class HipGPT:
+    def __init__(self, state_dict, cfg_gpt, device="cuda", dtype: str = "bf16", max_batch: int = 32,
+                 max_kv: Optional[int] = None):
+        assert dtype in ("bf16", "f32")
+        self.lib = _hip.load()
+        self.cfg = g = cfg_gpt
+        self.dev = torch.device(device)
+        self.mode = dtype
+        self.D, self.L, self.H = int(g.model_dim), int(g.layers), int(g.heads)
+        assert self.D == 64 * self.H, "kernels assume head size 64"
+        self.V = int(g.number_mel_codes)
+        self.start_text, self.stop_text = int(g.start_text_token), int(g.stop_text_token)
+        self.start_mel, self.stop_mel = int(g.start_mel_token), int(g.stop_mel_token)
+        self.max_kv = int(max_kv or (32 + int(g.max_text_tokens) + 2 + 1 + int(g.max_mel_tokens)))
+        sd = {k: _t(v) for k, v in state_dict.items()}
+        dev = self.dev
+        f32 = lambda k: sd[k].float().to(dev).contiguous()  # noqa: E731
+        self.sd_cond = {k: v.float().to(dev) for k, v in sd.items()
+                        if k.startswith(("conditioning_encoder", "perceiver_encoder"))}
+        self.text_emb, self.text_pos = f32("text_embedding.weight"), f32("text_pos_embedding.emb.weight")
+        self.mel_emb, self.mel_pos = f32("mel_embedding.weight"), f32("mel_pos_embedding.emb.weight")
+        self.ln_f = (f32("gpt.ln_f.weight"), f32("gpt.ln_f.bias"))
+        self.final_norm = (f32("final_norm.weight"), f32("final_norm.bias"))
+        self.layers: List[_Layer] = []
+        for i in range(self.L):
+            p = f"gpt.h.{i}"
+            ly = _Layer()
+            ly.ln1, ly.ln2 = (f32(p + ".ln_1.weight"), f32(p + ".ln_1.bias")), (f32(p + ".ln_2.weight"), f32(p + ".ln_2.bias"))
+            ly.b = {n: f32(f"{p}.{k}.bias") for n, k in
+                    (("qkv", "attn.c_attn"), ("o", "attn.c_proj"), ("fc", "mlp.c_fc"), ("proj", "mlp.c_proj"))}
+            ly.w = {}
+            for n, k in (("qkv", "attn.c_attn"), ("o", "attn.c_proj"), ("fc", "mlp.c_fc"), ("proj", "mlp.c_proj")):
+                wt = sd[f"{p}.{k}.weight"].float().t().contiguous()  # HF Conv1D [in, out] -> [out, in]
+                ly.w[n] = self._pack(wt)
+            self.layers.append(ly)
+        self.head_w = self._pack(sd["mel_head.weight"].float().contiguous(), igemm=False)
+        self.head_b = f32("mel_head.bias")
+        self._state = None
+        self._graph = None
+
+    # ---------------- weights ----------------
+    def _pack(self, wt: torch.Tensor, igemm: bool = True):
+        """wt: [N, K] f32 -> dict of device copies for the kernels of this mode."""
+        N, K = wt.shape
+        if self.mode == "f32":
+            return {"f32": wt.to(self.dev), "N": N, "K": K}
+        out = {"sk": pack_skinny(wt).to(self.dev), "N": N, "K": K}
+        if igemm:
+            from ..vocoder.bigvgan import pack_taps
+            out["ig"] = pack_taps([wt], K, N).to(self.dev)
+        return out
+
+    # ---------------- conditioning + inputs ----------------
+    @torch.no_grad()
+    def conditioning(self, mel: torch.Tensor, mel_lengths=None) -> torch.Tensor:
+        return get_conditioning(self.sd_cond, self.cfg, mel.to(self.dev).float(),
+                                None if mel_lengths is None else mel_lengths.to(self.dev))
+
+    def prepare_inputs(self, conds: torch.Tensor, text_ids: torch.Tensor):
+        """``prepare_gpt_inputs`` (gpt/model.py:591-654): strip ids 0/1, [0]+ids+[1], left zero pad.
+        -> emb [B, s+1, D] f32 (incl. the start-mel position), pad [B] int32, s."""
+        B, L = text_ids.shape
+        conds = conds.to(self.dev).float()
+        ncond = conds.shape[1]
+        s = ncond + L + 2
+        emb = torch.zeros(B, s + 1, self.D, device=self.dev)
+        pads = []
+        for i in range(B):
+            row = text_ids[i].to(self.dev).long()
+            row = row[(row != self.stop_text) & (row != self.start_text)]
+            row = torch.cat([row.new_tensor([self.start_text]), row, row.new_tensor([self.stop_text])])
+            te = self.text_emb[row] + self.text_pos[: row.numel()]
+            c = conds[0] if conds.shape[0] == 1 else conds[i]
+            pad = L + 2 - row.numel()
+            emb[i, pad:s] = torch.cat([c, te], 0)
+            pads.append(pad)
+        emb[:, s] = self.mel_emb[self.start_mel] + self.mel_pos[0]
+        return emb, torch.tensor(pads, dtype=torch.int32, device=self.dev), s
+
+    # ---------------- GEMM dispatch ----------------
+    def _gemm(self, A, w, Y=None, bias=None, gelu=False, residual=False, part=None, ksplit=1, skinny=False):
+        """Y = A @ W^T (+bias)(gelu)(+Y if residual); A [M, K].  skinny: decode-step weight-streaming
+        kernel (A rows padded to 32-row tiles; part = split-K f32 partials); else MFMA implicit GEMM."""
+        M, K = A.shape
+        N = w["N"]
+        st = _hip.stream_ptr()
+        if self.mode == "f32":
+            _hip.check(self.lib.itts_gemm_f32(A.data_ptr(), A.stride(0), w["f32"].data_ptr(), K, M, N, K,
+                                              _hip.ptr(bias), int(gelu), Y.data_ptr() if residual else None,
+                                              Y.data_ptr(), Y.stride(0), st), "itts_gemm_f32")
+            return
+        if not skinny:
+            _hip.check(self.lib.itts_igemm_fwd(A.data_ptr(), M * K, K, w["ig"].data_ptr(), _hip.ptr(bias), None,
+                                               Y.data_ptr() if residual else None, None, Y.data_ptr(), M * N,
+                                               Y.stride(0), None, 1, M, K, N, 1, _hip.i32_array([0]), 1, 0, 1.0,
+                                               int(gelu), _hip.dtype_code(Y), st), "itts_igemm_fwd")
+            return
+        assert not residual, "skinny path reduces residuals through itts_residual_reduce_ln"
+        _hip.check(self.lib.itts_skinny_gemm_bf16(
+            A.data_ptr(), A.stride(0), w["sk"].data_ptr(), K, N, M, _hip.ptr(bias) if part is None else None,
+            int(gelu), None if Y is None else Y.data_ptr(), 0 if Y is None else Y.stride(0),
+            BF16 if (Y is not None and Y.dtype == torch.bfloat16) else F32,
+            None if part is None else part.data_ptr(), N, ksplit, st), "itts_skinny_gemm_bf16")
+
+    def _ln(self, x, y, ln, ln2=None, idx=None, M=None):
+        M = x.shape[0] if M is None else M
+        _hip.check(self.lib.itts_layernorm_rows(
+            x.data_ptr(), x.stride(0), _hip.ptr(idx), y.data_ptr(), y.stride(0), M, self.D, ln[0].data_ptr(),
+            ln[1].data_ptr(), None if ln2 is None else ln2[0].data_ptr(), None if ln2 is None else ln2[1].data_ptr(),
+            _hip.dtype_code(y), _hip.stream_ptr()), "itts_layernorm_rows")
+
+    @property
+    def act_dtype(self):
+        return torch.bfloat16 if self.mode == "bf16" else torch.float32
+
+    # ---------------- full-sequence forward (prefill + latent pass) ----------------
+    def _forward_rows(self, x, seq_start, seq_len, seq_pad, max_len, cache=None):
+        """x [M, D] f32 (modified in place) through all layers; returns x (pre ln_f)."""
+        M, D = x.shape
+        ad = self.act_dtype
+        h = torch.empty(M, D, dtype=ad, device=self.dev)
+        qkv = torch.empty(M, 3 * D, dtype=torch.float32, device=self.dev)
+        o = torch.empty(M, D, dtype=ad, device=self.dev)
+        f = torch.empty(M, 4 * D, dtype=ad, device=self.dev)
+        st = _hip.stream_ptr()
+        cdt = _hip.dtype_code(cache[0]) if cache is not None else _hip.dtype_code(h)
+        for li, ly in enumerate(self.layers):
+            self._ln(x, h, ly.ln1)
+            self._gemm(h, ly.w["qkv"], qkv, bias=ly.b["qkv"])
+            ck = cv = None
+            cbs = chs = 0
+            if cache is not None:
+                ck, cv = cache[0][li], cache[1][li]
+                cbs, chs = ck.stride(0), ck.stride(1)
+            _hip.check(self.lib.itts_attn_prefill(
+                qkv.data_ptr(), 3 * D, seq_start.data_ptr(), seq_len.data_ptr(), _hip.ptr(seq_pad), seq_start.numel(),
+                max_len, _hip.ptr(ck), _hip.ptr(cv), cbs, chs, o.data_ptr(), D, self.H, cdt, _hip.dtype_code(o), st),
+                "itts_attn_prefill")
+            self._gemm(o, ly.w["o"], x, bias=ly.b["o"], residual=True)
+            self._ln(x, h, ly.ln2)
+            self._gemm(h, ly.w["fc"], f, bias=ly.b["fc"], gelu=True)
+            self._gemm(f, ly.w["proj"], x, bias=ly.b["proj"], residual=True)
+        return x
+
+    # ---------------- decode state ----------------
+    def _alloc_state(self, B: int, max_new: int):
+        D, dev = self.D, self.dev
+        Mp = (B + 31) // 32 * 32
+        ad = self.act_dtype
+        cdt = torch.bfloat16 if self.mode == "bf16" else torch.float32
+        st = {
+            "B": B, "Mp": Mp, "max_new": max_new,
+            "x": torch.zeros(B, D, device=dev),
+            "h": torch.zeros(Mp, D, dtype=ad, device=dev),
+            "qkv": torch.zeros(B, 3 * D, device=dev),
+            "o": torch.zeros(Mp, D, dtype=ad, device=dev),
+            "f": torch.zeros(Mp, 4 * D, dtype=ad, device=dev),
+            "part": torch.zeros(8, B, 4 * D, device=dev),
+            "logits": torch.zeros(B, self.V, device=dev),
+            "kc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
+            "vc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
+            "seen": torch.zeros(B, self.V, dtype=torch.uint8, device=dev),
+            "done": torch.zeros(B, dtype=torch.uint8, device=dev),
+            "codes": torch.full((B, max_new), self.stop_mel, dtype=torch.int32, device=dev),
+            "t": torch.zeros(4, dtype=torch.int32, device=dev),
+        }
+        return st
+
+    def _sample(self, st, col_delta, min_new, penalty):
+        _hip.check(self.lib.itts_sample_embed(
+            st["logits"].data_ptr(), self.V, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
+            st["codes"].data_ptr(), st["max_new"], st["t"].data_ptr(), col_delta, int(min_new), self.stop_mel,
+            float(penalty), self.mel_emb.data_ptr(), self.mel_pos.data_ptr(), 2, self.D,
+            self.layers[0].ln1[0].data_ptr(), self.layers[0].ln1[1].data_ptr(), st["x"].data_ptr(),
+            st["h"].data_ptr(), _hip.dtype_code(st["h"]), st["B"], _hip.ptr(st.get("forced")), _hip.stream_ptr()),
+            "itts_sample_embed")
+
+    def _decode_step(self, st, min_new, penalty):
+        """One fed token per row -> next token sampled (all device-side; graph-capturable)."""
+        B, D = st["B"], self.D
+        stream = _hip.stream_ptr()
+        x, h, qkv, o, f, part = st["x"], st["h"], st["qkv"], st["o"], st["f"], st["part"]
+        hB = h[:B]
+        for li, ly in enumerate(self.layers):
+            self._gemm(hB, ly.w["qkv"], qkv, bias=ly.b["qkv"], skinny=True)
+            kc, vc = st["kc"][li], st["vc"][li]
+            _hip.check(self.lib.itts_attn_decode(
+                qkv.data_ptr(), 3 * D, kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1), self.max_kv,
+                st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(), o.data_ptr(), D, B, self.H,
+                _hip.dtype_code(kc), _hip.dtype_code(o), stream), "itts_attn_decode")
+            nxt = self.layers[li + 1].ln1 if li + 1 < self.L else None
+            if self.mode == "f32":
+                self._gemm(o[:B], ly.w["o"], x, bias=ly.b["o"], residual=True)
+                self._ln(x, h, ly.ln2, M=B)
+                self._gemm(h[:B], ly.w["fc"], f, bias=ly.b["fc"], gelu=True)
+                self._gemm(f[:B], ly.w["proj"], x, bias=ly.b["proj"], residual=True)
+                if nxt is not None:
+                    self._ln(x, h, nxt, M=B)
+                else:
+                    self._ln(x, h, self.ln_f, self.final_norm, M=B)
+                continue
+            ko = self._ksplit(D)
+            self._gemm(o[:B], ly.w["o"], part=part, ksplit=ko, skinny=True)
+            self._reduce(st, ko, ly.b["o"], ly.ln2)
+            self._gemm(h[:B], ly.w["fc"], f, bias=ly.b["fc"], gelu=True, skinny=True)
+            kp = self._ksplit(4 * D)
+            self._gemm(f[:B], ly.w["proj"], part=part, ksplit=kp, skinny=True)
+            if nxt is not None:
+                self._reduce(st, kp, ly.b["proj"], nxt)
+            else:
+                self._reduce(st, kp, ly.b["proj"], self.ln_f, self.final_norm)
+        self._gemm(h[:B], self.head_w, st["logits"], bias=self.head_b, skinny=True)
+        self._sample(st, 1, min_new, penalty)
+        _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
+
+    @staticmethod
+    def _ksplit(K):
+        ks = K // 16
+        for s in (8, 4, 2):
+            if ks % s == 0 and ks // s >= 8:
+                return s
+        return 1
+
+    def _reduce(self, st, nsplit, bias, ln, ln2=None):
+        B, D = st["B"], self.D
+        part, x, h = st["part"], st["x"], st["h"]
+        _hip.check(self.lib.itts_residual_reduce_ln(
+            x.data_ptr(), D, part.data_ptr(), nsplit, B * D, D, bias.data_ptr(), h.data_ptr(), D, B, D,
+            ln[0].data_ptr(), ln[1].data_ptr(), None if ln2 is None else ln2[0].data_ptr(),
+            None if ln2 is None else ln2[1].data_ptr(), _hip.dtype_code(h), _hip.stream_ptr()),
+            "itts_residual_reduce_ln")
+
+    # ---------------- public: greedy generate ----------------
+    @torch.no_grad()
+    def generate(self, conds: torch.Tensor, text_ids: torch.Tensor, max_new_tokens: int,
+                 repetition_penalty: float = 10.0, min_new_tokens: int = 0, use_graph: bool = True,
+                 check_every: int = 16, forced_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Greedy decode (do_sample=False, num_beams=1) -> codes [B, n] int64 on the device, finished
+        rows padded with the stop token, n = steps until every row stopped (or max_new_tokens)."""
+        emb, pad, s = self.prepare_inputs(conds, text_ids)
+        B = emb.shape[0]
+        assert s + 1 + max_new_tokens <= self.max_kv, "KV capacity exceeded"
+        key = (B, max_new_tokens, s)
+        if self._state is None or self._state["key"] != key:
+            self._state = self._alloc_state(B, max_new_tokens)
+            self._state["key"] = key
+            self._graph = None
+        st = self._state
+        st["s"] = s
+        st["pad"] = pad
+        st["seen"].zero_()
+        st["seen"][:, 1] = 1
+        st["seen"][:, self.start_mel] = 1
+        st["done"].zero_()
+        st["t"].zero_()
+        st["codes"].fill_(self.stop_mel)
+        if forced_codes is not None:  # teacher forcing (tests): feed these ids, record the argmax ids
+            fc = torch.full((B, max_new_tokens), self.stop_mel, dtype=torch.int32, device=self.dev)
+            fc[:, : forced_codes.shape[1]] = forced_codes.to(self.dev, torch.int32)
+            if st.get("forced") is None or st["forced"].shape != fc.shape:
+                st["forced"] = fc
+                self._graph = None
+            else:
+                st["forced"].copy_(fc)
+        elif st.get("forced") is not None:
+            st["forced"] = None
+            self._graph = None
+        # ---- prefill over [B, s+1] rows ----
+        M = B * (s + 1)
+        x = emb.reshape(M, self.D).contiguous()
+        starts = torch.arange(B, dtype=torch.int32, device=self.dev) * (s + 1)
+        lens = torch.full((B,), s + 1, dtype=torch.int32, device=self.dev)
+        self._forward_rows(x, starts, lens, pad, s + 1, cache=(st["kc"], st["vc"]))
+        last = (starts + s).contiguous()
+        self._ln(x, st["h"], self.ln_f, self.final_norm, idx=last, M=B)
+        self._gemm(st["h"][:B], self.head_w, st["logits"], bias=self.head_b, skinny=True)
+        self._sample(st, 0, min_new_tokens, repetition_penalty)
+        # ---- decode loop ----
+        steps = 1
+        graph_ok = use_graph and self._graph is not None and self._graph[1] == (min_new_tokens, repetition_penalty)
+        if use_graph and not graph_ok and max_new_tokens > 1:
+            self._capture(st, min_new_tokens, repetition_penalty)
+            graph_ok = True
+        while steps < max_new_tokens:
+            if graph_ok:
+                self._graph[0].replay()
+            else:
+                self._decode_step(st, min_new_tokens, repetition_penalty)
+            steps += 1
+            if steps % check_every == 0 and bool(st["done"].all()):
+                break
+        codes = st["codes"][:, :steps].long()
+        hit = codes == self.stop_mel
+        if bool(hit.any(dim=1).all()):
+            n = int(hit.int().argmax(dim=1).max()) + 1
+            codes = codes[:, :n]
+        return codes
+
+    def _capture(self, st, min_new, penalty):
+        """Capture one decode step into a hipGraph; counters are device-side so replays advance."""
+        t_save = st["t"].clone()
+        x_save, h_save = st["x"].clone(), st["h"].clone()
+        seen_save, done_save, codes_save = st["seen"].clone(), st["done"].clone(), st["codes"].clone()
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            self._decode_step(st, min_new, penalty)  # warm-up (also validates launches)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        # restore state mutated by the warm-up step
+        st["t"].copy_(t_save); st["x"].copy_(x_save); st["h"].copy_(h_save)
+        st["seen"].copy_(seen_save); st["done"].copy_(done_save); st["codes"].copy_(codes_save)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._decode_step(st, min_new, penalty)
+        self._graph = (g, (min_new, penalty))
+        # capture does not execute the kernels; state is intact
+
+    # ---------------- latent pass ----------------
+    @torch.no_grad()
+    def latent(self, conds: torch.Tensor, text_list: List[torch.Tensor], codes_list: List[torch.Tensor]):
+        """Teacher-forced pass for each utterance (gpt/model.py:521-578, return_latent=True).
+
+        conds [B|1, 32, D]; text_list[b] = ids [L_b] (used as given); codes_list[b] = codes [n_b]
+        -> (latent [B, Tmax, D] in the vocoder's input layout (bf16 in bf16 mode), lengths [B])."""
+        B = len(text_list)
+        conds = conds.to(self.dev).float()
+        rows, starts, lens, mel_rows = [], [], [], []
+        M = 0
+        for b in range(B):
+            t = text_list[b].to(self.dev).long().reshape(-1)
+            c = codes_list[b].to(self.dev).long().reshape(-1)
+            t = torch.cat([t.new_tensor([self.start_text]), t, t.new_tensor([self.stop_text])])
+            m = torch.cat([c.new_tensor([self.start_mel]), c, c.new_tensor([self.stop_mel])])
+            cb = conds[0] if conds.shape[0] == 1 else conds[b]
+            x = torch.cat([cb, self.text_emb[t] + self.text_pos[: t.numel()],
+                           self.mel_emb[m] + self.mel_pos[: m.numel()]], 0)
+            rows.append(x)
+            starts.append(M)
+            lens.append(x.shape[0])
+            first = M + cb.shape[0] + t.numel()
+            mel_rows.append(torch.arange(first, first + c.numel(), device=self.dev))
+            M += x.shape[0]
+        x = torch.cat(rows, 0).contiguous()
+        s_t = torch.tensor(starts, dtype=torch.int32, device=self.dev)
+        l_t = torch.tensor(lens, dtype=torch.int32, device=self.dev)
+        self._forward_rows(x, s_t, l_t, None, max(lens))
+        n = [int(c.numel()) for c in codes_list]
+        Tmax = max(n)
+        idx = torch.zeros(B, Tmax, dtype=torch.int32, device=self.dev)
+        for b in range(B):
+            idx[b, : n[b]] = mel_rows[b].int()
+        out = torch.empty(B, Tmax, self.D, dtype=self.act_dtype, device=self.dev)
+        self._ln(x, out.view(B * Tmax, self.D), self.ln_f, self.final_norm, idx=idx.view(-1), M=B * Tmax)
+        return out, torch.tensor(n, dtype=torch.int32)
+
+
+F32, BF16 = _hip.F32, _hip.BF16
