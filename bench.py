@@ -1,0 +1,224 @@
+#!/usr/bin/env python
+"""IndexTTS-1.5 hot-path throughput on MI355X: audio-seconds per wall-second (BASELINE.json metric).
+
+One "step" = one batch of B=32 zero-shot utterances per GPU (config C3): per-prompt conditioning +
+ECAPA speaker embedding for 32 distinct prompt mels (511 frames), GPT prefill + 400 greedy decode
+steps (EOS suppressed, hipGraph-replayed) at repetition_penalty 10, remove_long_silence, the
+teacher-forced latent pass, BigVGAN2 -> int16 PCM; with N>1 ranks the finished waveforms are gathered
+to rank 0 over RCCL (utterances shard data-parallel, weak scaling).  Inputs are resident in HBM when
+the timed region starts; weights are seeded random-init IndexTTS-1.5 (no checkpoints are available).
+
+Also reports, for the dominant kernel (the MFMA implicit-GEMM that runs every BigVGAN conv), its
+achieved TFLOP/s from HIP events over the timed region, and a CPU baseline: the fp32 oracle (a CPU
+restatement of the reference path) on a bounded sample, on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "index-tts-dubbing_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "audio-seconds/sec/GPU (RTF) IndexTTS-1.5 bf16 batch=32; 1→8 GPU scaling"
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+class KernelTimer:
+    """HIP-event timing of every launch of one kernel family, on the stream it is launched on."""
+
+    def __init__(self):
+        self.events = []
+        self.flops = 0.0
+        self.launches = 0
+        self.enabled = False
+
+    def wrap(self, fn, flops):
+        if not self.enabled:
+            return fn()
+        s = torch.cuda.current_stream()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        r = fn()
+        b.record(s)
+        self.events.append((a, b))
+        self.flops += flops
+        self.launches += 1
+        return r
+
+    def result(self):
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in self.events)
+        return ms, self.flops, self.launches
+
+
+def install_conv_timer(voc, timer):
+    orig = voc._conv
+
+    def timed(c, x, y, lens, **kw):
+        rows = voc.rows  # host-side count of valid rows (no device sync)
+        return timer.wrap(lambda: orig(c, x, y, lens, **kw), 2.0 * rows * c.cout * c.cin * c.ntaps)
+
+    voc._conv = timed
+
+
+def make_inputs(cfg, rank, B, L, frames):
+    mels, texts = [], []
+    for i in range(B):
+        g = np.random.default_rng(2 + rank * B + i)
+        mels.append(torch.from_numpy(g.normal(-4.0, 2.0, (1, 100, frames)).astype(np.float32)))
+        texts.append(torch.from_numpy(g.integers(2, int(cfg.gpt.number_text_tokens), L).astype(np.int64)))
+    return mels, texts
+
+
+def cpu_baseline(cfg, gsd, vsd, B, N, L, frames):
+    """fp32 oracle (CPU restatement of the reference path) on a bounded sample: B utterances x N codes."""
+    from indextts.gpt.conditioning import get_conditioning
+    from indextts.vocoder.ecapa import speaker_embedding
+    from oracle.bigvgan_oracle import BigVGANOracle, fold_weight_norm
+    from oracle.gpt_oracle import GPTOracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    gt = {k: torch.from_numpy(np.asarray(v)) for k, v in gsd.items()}
+    orc = GPTOracle(gt, cfg.gpt)
+    voc = BigVGANOracle(vsd, cfg.bigvgan)
+    vt = {k: v for k, v in fold_weight_norm(vsd).items()}
+    mels, texts = make_inputs(cfg, 0, B, L, frames)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        mel = torch.cat(mels, 0)
+        conds = get_conditioning(gt, cfg.gpt, mel)
+        spk = speaker_embedding(vt, mel.transpose(1, 2))
+        codes = orc.generate(conds, torch.stack(texts), N, min_new_tokens=N)
+        audio = 0.0
+        for b in range(B):
+            fixed, _ = orc.remove_long_silence(codes[b:b + 1])
+            lat = orc.latent(conds[b:b + 1], texts[b][None], fixed)
+            wav = voc.forward(lat, spk[b:b + 1])
+            audio += wav.shape[-1] / 24000.0
+        dt = time.perf_counter() - t0
+    return {"value": round(audio / dt, 4), "unit": "audio-seconds/sec", "cores": threads, "kind": "port",
+            "sample": f"{B} utterances x {N} codes (L={L}, {frames}-frame prompts), fp32 oracle incl. conditioning, "
+                      f"ECAPA, greedy decode, latent pass and vocoder; {audio:.2f} audio-s in {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--codes", type=int, default=400)
+    ap.add_argument("--text-len", type=int, default=48)
+    ap.add_argument("--prompt-frames", type=int, default=511)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--cpu-codes", type=int, default=32)
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from indextts.pipeline import BatchedTTS, SR
+    from indextts.utils.config import default_config_path, load_config
+    from indextts.utils.synthetic import bigvgan_state_dict, gpt_state_dict
+
+    cfg = load_config(default_config_path())
+    gsd = gpt_state_dict(cfg.gpt, seed=0, mel_head_std=0.08)
+    vsd = bigvgan_state_dict(cfg.bigvgan, seed=0)
+    B, N, L = args.batch, args.codes, args.text_len
+    tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + L + 2 + 1 + N + 8)
+    timer = KernelTimer()
+    install_conv_timer(tts.vocoder, timer)
+    mels, texts = make_inputs(cfg, rank, B, L, args.prompt_frames)
+    mels = [m.to(dev) for m in mels]
+    texts = [t.to(dev) for t in texts]
+
+    def step():
+        pcm, lens, _ = tts.synthesize(mels, texts, max_mel_tokens=N, min_new_tokens=N)
+        if world > 1:
+            raw = pcm.contiguous().view(torch.uint8).reshape(-1)
+            n = torch.tensor([raw.numel()], device=dev, dtype=torch.int64)
+            sizes = [torch.zeros_like(n) for _ in range(world)]
+            dist.all_gather(sizes, n)
+            cap = int(max(int(s) for s in sizes))
+            buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+            buf[: raw.numel()] = raw
+            gl = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+            dist.gather(buf, gl, dst=0)
+        return float(lens.sum()) / SR
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.enabled = not args.no_kernel_timing
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    audio = 0.0
+    for _ in range(args.steps):
+        audio += step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    timer.enabled = False
+    k_ms, k_flops, k_n = timer.result()
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+        a = torch.tensor([audio], device=dev, dtype=torch.float64)
+        dist.all_reduce(a, op=dist.ReduceOp.SUM)
+        audio = float(a)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    achieved = (k_flops / (k_ms * 1e-3) / 1e12) if k_ms > 0 else None
+    roof = {"kernel": "itts_igemm_fwd (BigVGAN convs, MFMA bf16)", "bound": "mfma",
+            "achieved": None if achieved is None else round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / PEAK_BF16_TFLOPS, 4),
+            "traffic": None, "launches": k_n, "avg_launch_us": round(1e3 * k_ms / max(k_n, 1), 2),
+            "share_of_step": round(k_ms / (1e3 * dt), 3)}
+    tf = os.path.join(REPO, "profiles", "traffic_r01.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            roof["traffic"] = json.load(f).get("igemm_bytes_per_launch")
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(cfg, gsd, vsd, args.cpu_batch, args.cpu_codes, L, args.prompt_frames)
+    out = {
+        "metric": METRIC, "value": round(audio / dt, 3), "unit": "audio-seconds/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic: seeded random-init IndexTTS-1.5 weights, random 511-frame prompt mels, random text ids",
+        "config": {"workload": f"C3: batch={B} zero-shot utterances per GPU (one prompt each), L={L} text ids, "
+                               f"{N} codes each (EOS suppressed): conditioning+ECAPA, GPT prefill+decode (hipGraph), "
+                               "latent pass, BigVGAN2 -> int16", "global_batch": B * world, "seq_len": N,
+                   "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -210,6 +210,7 @@ class HipGPT:
             "done": torch.zeros(B, dtype=torch.uint8, device=dev),
             "codes": torch.full((B, max_new), self.stop_mel, dtype=torch.int32, device=dev),
             "t": torch.zeros(4, dtype=torch.int32, device=dev),
+            "pad": torch.zeros(B, dtype=torch.int32, device=dev),  # graph-captured pointer: update in place
         }
         return st
 
@@ -294,7 +295,7 @@ class HipGPT:
             self._graph = None
         st = self._state
         st["s"] = s
-        st["pad"] = pad
+        st["pad"].copy_(pad)  # never rebind: the captured graph holds this pointer
         st["seen"].zero_()
         st["seen"][:, 1] = 1
         st["seen"][:, self.start_mel] = 1

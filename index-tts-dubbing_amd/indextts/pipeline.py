@@ -1,0 +1,88 @@
+"""Batched IndexTTS hot path: conditioning -> GPT greedy decode -> remove_long_silence -> latent pass
+-> BigVGAN2 -> int16 PCM, for many utterances at once on one GPU.
+
+The reference runs this chain one sentence at a time (``IndexTTS.infer``, ``indextts/infer.py:553-631``)
+or in buckets of <= 4 (``infer_fast``); here a whole batch (32 by default) shares every launch, and each
+utterance's result equals what it produces alone (per-row decode state, per-utterance lengths in the
+latent pass and the vocoder).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .gpt.engine import HipGPT
+from .vocoder.bigvgan import HipBigVGAN
+
+HOP = 1024
+SR = 24000
+
+
+def remove_long_silence(codes: np.ndarray, stop: int, silent_token: int = 52, max_consecutive: int = 30):
+    """``IndexTTS.remove_long_silence`` (infer.py:132-186) for one row -> kept codes (1-D int64)."""
+    hits = np.nonzero(codes == stop)[0]
+    n = int(hits[0]) if len(hits) else codes.shape[0]
+    if int((codes == silent_token).sum()) > max_consecutive:
+        keep, run = [], 0
+        for k in range(n):
+            if codes[k] != silent_token:
+                keep.append(k)
+                run = 0
+            elif run < 10:
+                keep.append(k)
+                run += 1
+        return codes[keep]
+    return codes[:n]
+
+
+class BatchedTTS:
+    def __init__(self, gpt_state_dict, bigvgan_state_dict, cfg, device="cuda", dtype: str = "bf16",
+                 max_kv: Optional[int] = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.gpt = HipGPT(gpt_state_dict, cfg.gpt, device, dtype=dtype, max_kv=max_kv)
+        self.vocoder = HipBigVGAN(bigvgan_state_dict, cfg.bigvgan, device)
+        self.stop = int(cfg.gpt.stop_mel_token)
+        self.stop_text = int(cfg.gpt.stop_text_token)
+        self._prompt_cache: Dict[object, tuple] = {}
+
+    @torch.no_grad()
+    def prompt_features(self, mels: Sequence[torch.Tensor], keys: Optional[Sequence[object]] = None):
+        """per-prompt conditioning (conds [32, D]) and speaker embedding ([spk_dim]); cached by key."""
+        feats: Dict[int, tuple] = {}
+        todo = [i for i in range(len(mels)) if keys is None or keys[i] not in self._prompt_cache]
+        by_len: Dict[int, List[int]] = {}  # equal-length prompts share one batched call
+        for i in todo:
+            by_len.setdefault(int(mels[i].shape[-1]), []).append(i)
+        for idx in by_len.values():
+            m = torch.cat([mels[i].reshape(1, mels[i].shape[-2], mels[i].shape[-1]) for i in idx], 0).to(self.device)
+            c = self.gpt.conditioning(m)
+            s = self.vocoder.speaker(m.transpose(1, 2))
+            for j, i in enumerate(idx):
+                feats[i] = (c[j], s[j])
+                if keys is not None:
+                    self._prompt_cache[keys[i]] = feats[i]
+        vals = [feats[i] if i in feats else self._prompt_cache[keys[i]] for i in range(len(mels))]
+        return torch.stack([v[0] for v in vals]), torch.stack([v[1] for v in vals])
+
+    @torch.no_grad()
+    def synthesize(self, mels: Sequence[torch.Tensor], texts: Sequence[torch.Tensor], max_mel_tokens: int = 600,
+                   repetition_penalty: float = 10.0, min_new_tokens: int = 0, keys=None, use_graph: bool = True):
+        """mels[b]: prompt log-mel [1, 100, T_b]; texts[b]: token ids [L_b].
+        -> (pcm int16 [B, Tmax] on device, sample lengths [B] (cpu), codes list)."""
+        B = len(texts)
+        conds, spk = self.prompt_features(mels, keys)
+        L = max(int(t.numel()) for t in texts)
+        ids = torch.full((B, L), self.stop_text, dtype=torch.long)
+        for b, t in enumerate(texts):
+            ids[b, : t.numel()] = t.reshape(-1).long()
+        codes = self.gpt.generate(conds, ids.to(self.device), max_mel_tokens, repetition_penalty=repetition_penalty,
+                                  min_new_tokens=min_new_tokens, use_graph=use_graph)
+        rows = codes.cpu().numpy()
+        fixed = [torch.from_numpy(remove_long_silence(rows[b], self.stop)) for b in range(B)]
+        fixed = [f if f.numel() > 0 else torch.tensor([self.stop]) for f in fixed]  # degenerate: nothing generated
+        latent, lens = self.gpt.latent(conds, [t.reshape(-1) for t in texts], fixed)
+        _, pcm = self.vocoder.forward(latent, lens, spk)
+        return pcm, (lens.long() * HOP), fixed

@@ -205,6 +205,7 @@ class HipBigVGAN:
             x = x.to(torch.bfloat16)
         x = x.contiguous()
         B, T, _ = x.shape
+        self.rows = int(lengths.sum())  # valid input rows of the current conv (host-side, for FLOP accounting)
         lens = lengths.to(dev, torch.int32).contiguous()
         pre_b, stage_b = self.cond_biases(spk.to(dev))
         C0 = self.conv_pre.cout
@@ -218,6 +219,7 @@ class HipBigVGAN:
             x_st = self._buf("x", (B, Tn, C))
             for rho, ph in enumerate(phases):
                 self._conv(ph, cur_in, x_st, lens, bias_b=stage_b[i], ymul=u, yoff=rho)
+            self.rows *= u
             t1 = self._buf("t1", (B, Tn, C))
             t2 = self._buf("t2", (B, Tn, C))
             cur = self._buf("cur", (B, Tn, C))

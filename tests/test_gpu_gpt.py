@@ -161,3 +161,21 @@ def test_bf16_batch32_runs_and_is_batch_invariant(golden):
     for i in (0, 7, 31):
         one = eng.generate(conds, text[i:i + 1, : rows[i].numel()], 20, min_new_tokens=20).cpu()
         assert torch.equal(one[0], out[i]), i
+
+
+def test_graph_replay_across_calls_matches_eager(golden):
+    """A captured decode graph is reused by later generate() calls with the same shapes; every
+    device buffer it references must be updated in place (regression: stale pad pointer)."""
+    eng = _engine("tiny", "bf16")
+    conds = torch.from_numpy(golden["tiny_gpt_conds"]).cuda()
+    g = torch.Generator().manual_seed(9)
+    outs = []
+    for call in range(3):
+        text = torch.randint(2, 12000, (4, 10), generator=g)
+        text[call % 4, :3] = 0  # different left padding per call
+        text = text.cuda()
+        a = eng.generate(conds, text, 12, min_new_tokens=12, use_graph=True).cpu()
+        b = eng.generate(conds, text, 12, min_new_tokens=12, use_graph=False).cpu()
+        assert torch.equal(a, b), call
+        outs.append(a)
+    assert not torch.equal(outs[0], outs[1])
