@@ -201,6 +201,10 @@ def main():
         with open(tf) as f:
             roof["traffic"] = json.load(f).get("igemm_bytes_per_launch")
     cpu = None
+    if args.breakdown:
+        ph = {}
+        step_t = tts.synthesize(mels, texts, max_mel_tokens=N, min_new_tokens=N, timings=ph)
+        print("breakdown (s):", json.dumps({k: round(v, 4) for k, v in ph.items()}), file=sys.stderr, flush=True)
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(cfg, gsd, vsd, args.cpu_batch, args.cpu_codes, L, args.prompt_frames)
     out = {

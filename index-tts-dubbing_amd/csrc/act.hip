@@ -34,7 +34,7 @@ struct ActArgs {
 };
 
 __device__ __forceinline__ float snake(float u, float a, float inv_b) {
-  float s = sinf(u * a);
+  float s = __sinf(u * a);  // v_sin_f32 (range-reduced in revolutions); accurate sinf was ~2x the kernel time
   return u + inv_b * (s * s);
 }
 

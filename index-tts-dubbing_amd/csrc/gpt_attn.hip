@@ -79,28 +79,33 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
 #pragma unroll
   for (int e = 0; e < 8; ++e) q[e] = qs[8 * d8 + e];
   // scores for keys p0 .. kidx (the new key from LDS so the just-written cache line is never re-read)
+  // KB key rows per 8-lane group per round, all loads issued before use (latency hiding)
+  constexpr int KB = 8;
   float lmax = -INFINITY;
-  for (int j0 = 0; j0 < nk; j0 += 32) {
-    const int j = j0 + g;
-    float part = 0.f;
-    if (j < nk) {
-      float k[8];
-      if (p0 + j == kidx) {
+  for (int j0 = 0; j0 < nk; j0 += 32 * KB) {
+    float k[KB][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) k[e] = kn[8 * d8 + e];
-      } else {
-        load8<TC>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8, k);
-      }
+    for (int u = 0; u < KB; ++u) {
+      const int j = j0 + 32 * u + g;
+      if (j < nk && p0 + j != kidx) load8<TC>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8, k[u]);
+      else
 #pragma unroll
-      for (int e = 0; e < 8; ++e) part = fmaf(q[e], k[e], part);
+        for (int e = 0; e < 8; ++e) k[u][e] = kn[8 * d8 + e];
     }
-    part += __shfl_xor(part, 1, 64);
-    part += __shfl_xor(part, 2, 64);
-    part += __shfl_xor(part, 4, 64);
-    if (j < nk && d8 == 0) {
-      const float s = part * 0.125f;
-      sc[j] = s;
-      lmax = fmaxf(lmax, s);
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int j = j0 + 32 * u + g;
+      float part = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part = fmaf(q[e], k[u][e], part);
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      part += __shfl_xor(part, 4, 64);
+      if (j < nk && d8 == 0) {
+        const float s = part * 0.125f;
+        sc[j] = s;
+        lmax = fmaxf(lmax, s);
+      }
     }
   }
   const float mx = block_reduce(lmax, red, true);
@@ -112,17 +117,23 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
   }
   const float inv = 1.0f / block_reduce(lsum, red, false);  // includes a barrier: sc[] complete
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j = g; j < nk; j += 32) {
-    float v[8];
-    if (p0 + j == kidx) {
+  for (int j0 = 0; j0 < nk; j0 += 32 * KB) {
+    float v[KB][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = vn[8 * d8 + e];
-    } else {
-      load8<TC>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8, v);
+    for (int u = 0; u < KB; ++u) {
+      const int j = j0 + 32 * u + g;
+      if (j < nk && p0 + j != kidx) load8<TC>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8, v[u]);
+      else
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[u][e] = vn[8 * d8 + e];
     }
-    const float p = sc[j];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = fmaf(p, v[e], o[e]);
+    for (int u = 0; u < KB; ++u) {
+      const int j = j0 + 32 * u + g;
+      const float p = j < nk ? sc[j] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(p, v[u][e], o[e]);
+    }
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) pv[g][8 * d8 + e] = o[e];

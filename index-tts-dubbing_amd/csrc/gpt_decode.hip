@@ -1,0 +1,272 @@
+// Fused decode-step projection GEMM for gfx950 (batch rows M <= 32 per launch tile).
+//
+//   Y = epi( prologue(X) @ W^T )
+//     prologue: A = X (bf16 [M][K], global)                      -- LNMODE 0
+//               A = LN_1(X) (X f32 residual stream [M][K])         -- LNMODE 1  (HF ln_1 / ln_2)
+//               A = LN_2(LN_1(X))                                  -- LNMODE 2  (ln_f then final_norm, Q5)
+//     epilogue: EPI 0: Y = act(acc + bias) stored as OutT (act = gelu_tanh optional)
+//               EPI 1: Y(f32) += acc + bias                        (residual add, in place)
+//               EPI 2: Y[ks] = acc  (f32 partial of K split ks; reduced + LayerNormed by
+//                      itts_residual_reduce_ln in gpt_norm.hip -- deterministic, no atomics)
+//
+// Product decode step (engine.HipGPT._decode_step) uses LNMODE 0 everywhere: the residual add and
+// the following LayerNorm are fused into one reduce kernel per sub-layer, and the O / MLP-proj
+// GEMMs (K = D or 4D, N = D: only D/32 column tiles) are split along K so that >= 256 workgroups
+// stream the weights.  LNMODE 1/2 (LayerNorm recomputed per workgroup from the L2-resident
+// residual stream, staged in LDS as bf16) measured slower at batch 32 and is kept for small-D
+// models and the unit tests.
+//
+// Weights are prepacked in MFMA-fragment order [N/32][K/16][64][8] bf16 (see pack_skinny): one
+// wave load = one contiguous 1 KiB line pair.  Workgroup = NW waves over interleaved k-steps,
+// 2-stage register pipeline (next 8 k-steps' loads issued before this batch's MFMAs), fixed-order
+// cross-wave reduction through LDS (bitwise batch-invariant per row).
+#include "common.h"
+
+namespace {
+
+constexpr int kU = 8;
+
+__device__ __forceinline__ float gelu_tanh_d(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+template <int NW>
+__device__ __forceinline__ float wg_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += red[i];
+  return s;
+}
+
+struct DgArgs {
+  const void* a;      // LNMODE 0: bf16 A [.][lda]; else f32 X [.][lda]
+  int64_t lda;
+  const u32x4_t* w;   // packed weights
+  int K, N, M;
+  const float* bias;
+  const float *g1, *b1, *g2, *b2;
+  int gelu;
+  void* y;
+  int64_t ldy;
+  int64_t split_stride;  // EPI 2: floats between the partial products of consecutive K splits
+};
+
+// normalise RPW rows held in registers (one wave, 64 lanes x KPL elements per row)
+template <int KPL>
+__device__ __forceinline__ void ln_vec(float (&v)[KPL], const float* g, const float* b, int K) {
+  const int lane = threadIdx.x & 63;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) s += v[i];
+  const float mean = wave_sum(s) / K;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) q += (v[i] - mean) * (v[i] - mean);
+  const float rstd = rsqrtf(wave_sum(q) / K + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < KPL / 4; ++i) {
+    const int e = 4 * (lane + 64 * i);
+    const f32x4_t g4 = *reinterpret_cast<const f32x4_t*>(g + e);
+    const f32x4_t b4 = *reinterpret_cast<const f32x4_t*>(b + e);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * i + j] = (v[4 * i + j] - mean) * rstd * g4[j] + b4[j];
+  }
+}
+
+// EPI: 0 store act(acc + bias) as OutT; 1 f32 Y += acc + bias; 2 split-K over gridDim.y, each split
+// stores its f32 partial product (an in-kernel last-arriver reduction was measured slower: the two
+// agent-scope fences it needs cost more than the separate reduce launch).
+template <int NW, int LNMODE, int EPI, int KLN, typename OutT>
+__global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
+  constexpr int APITCH = KLN * 2 + 16;  // LDS row pitch (bytes) of the normalised A tile
+  constexpr int RED_BYTES = NW * 16 * 64 * sizeof(float);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* red = reinterpret_cast<float*>(smem);                 // [NW][16][64] f32
+  unsigned char* As = smem + RED_BYTES;                         // [32][APITCH] bf16 (LN modes)
+  const int nt = blockIdx.x, ks = blockIdx.y, nsplit = gridDim.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int K = LNMODE ? KLN : p.K;
+  const int ksteps = K / 16, kper = ksteps / nsplit, kbeg = ks * kper;
+  const int niter = (kper - w + NW - 1) / NW;  // this wave's k-steps: kbeg + w + NW*i
+  const u32x4_t* Wt = p.w + ((int64_t)nt * ksteps + kbeg) * 64 + lane;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  // zero-initialised: guarded (i < niter) MFMAs on never-loaded slots were speculated by hipcc and
+  // produced NaN columns for short K (measured: K=256/512) -- keep every slot defined
+  u32x4_t wa[kU] = {}, wb[kU] = {};
+  auto wload = [&](u32x4_t (&dst)[kU], int i0) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u < niter) dst[u] = __builtin_nontemporal_load(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
+  };
+  wload(wa, 0);  // weight stream starts before the prologue
+
+  if (LNMODE) {
+    // wave w normalises rows w + NW*j (j < 32/NW); all row loads issued before the first reduction
+    constexpr int KPL = KLN / 64, RPW = 32 / NW;
+    const float* X = reinterpret_cast<const float*>(p.a);
+    float v[RPW][KPL];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int r = w + NW * j;
+#pragma unroll
+      for (int i = 0; i < KPL / 4; ++i) {
+        f32x4_t x4 = {0.f, 0.f, 0.f, 0.f};
+        if (r < p.M) x4 = *reinterpret_cast<const f32x4_t*>(X + (int64_t)r * p.lda + 4 * (lane + 64 * i));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][4 * i + e] = x4[e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int r = w + NW * j;
+      if (r < p.M) {  // wave-uniform
+        ln_vec<KPL>(v[j], p.g1, p.b1, KLN);
+        if (LNMODE == 2) ln_vec<KPL>(v[j], p.g2, p.b2, KLN);
+      }
+#pragma unroll
+      for (int i = 0; i < KPL / 4; ++i) {
+        const u32x2_t pk = {pack2bf(v[j][4 * i], v[j][4 * i + 1]), pack2bf(v[j][4 * i + 2], v[j][4 * i + 3])};
+        *reinterpret_cast<u32x2_t*>(As + r * APITCH + 8 * (lane + 64 * i)) = pk;
+      }
+    }
+    __syncthreads();
+  }
+
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  auto afrag = [&](int s) -> bf16x8_t {
+    if (LNMODE) return *reinterpret_cast<const bf16x8_t*>(As + r32 * APITCH + 32 * s + 16 * h);
+    const uint16_t* A = reinterpret_cast<const uint16_t*>(p.a);
+    return *reinterpret_cast<const bf16x8_t*>(A + (int64_t)r32 * p.lda + 16 * s + 8 * h);
+  };
+  auto compute = [&](const u32x4_t (&src)[kU], int i0) {
+    bf16x8_t af[kU] = {};
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u < niter) af[u] = afrag(kbeg + w + NW * (i0 + u));
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u < niter)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[u], *reinterpret_cast<const bf16x8_t*>(&src[u]), acc, 0, 0, 0);
+  };
+  for (int i0 = 0; i0 < niter; i0 += 2 * kU) {
+    if (i0 + kU < niter) wload(wb, i0 + kU);
+    compute(wa, i0);
+    if (i0 + 2 * kU < niter) wload(wa, i0 + 2 * kU);
+    if (i0 + kU < niter) compute(wb, i0 + kU);
+  }
+
+  float* myred = red + w * 16 * 64;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) myred[r * 64 + lane] = acc[r];
+  __syncthreads();
+  constexpr int PER = 1024 / (64 * NW);  // tile outputs per thread
+  float tv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int o = threadIdx.x + 64 * NW * k;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v += red[ww * 1024 + o];
+    tv[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int o = threadIdx.x + 64 * NW * k;
+    const int r = o / 64, l = o % 64;
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+    const int n = nt * 32 + (l & 31);
+    if (row >= p.M || n >= p.N) continue;
+    if (EPI == 2) {  // split-K partial (no bias); reduced in fixed order by itts_residual_reduce_ln
+      reinterpret_cast<float*>(p.y)[ks * p.split_stride + (int64_t)row * p.ldy + n] = tv[k];
+      continue;
+    }
+    float v = tv[k];
+    if (p.bias) v += p.bias[n];
+    if (EPI >= 1) {
+      float* Y = reinterpret_cast<float*>(p.y) + (int64_t)row * p.ldy + n;
+      *Y = *Y + v;
+    } else {
+      if (p.gelu) v = gelu_tanh_d(v);
+      St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
+    }
+  }
+}
+
+template <int NW, int LNMODE, int EPI, int KLN, typename OutT>
+void launch_dg(const DgArgs& a, int row_tiles, int ksplit, hipStream_t s) {
+  size_t lds = NW * 16 * 64 * sizeof(float) + (LNMODE ? 32 * (KLN * 2 + 16) : 0);
+  for (int t = 0; t < row_tiles; ++t) {
+    DgArgs b = a;
+    const int64_t ra = (int64_t)t * 32;
+    b.M = a.M - 32 * t < 32 ? a.M - 32 * t : 32;
+    if (LNMODE) b.a = reinterpret_cast<const float*>(a.a) + ra * a.lda;
+    else b.a = reinterpret_cast<const uint16_t*>(a.a) + ra * a.lda;
+    if (EPI >= 1) b.y = reinterpret_cast<float*>(a.y) + ra * a.ldy;
+    else b.y = reinterpret_cast<OutT*>(a.y) + ra * a.ldy;
+    hipLaunchKernelGGL((decode_gemm_kernel<NW, LNMODE, EPI, KLN, OutT>), dim3((a.N + 31) / 32, ksplit), dim3(64 * NW),
+                       lds, s, b);
+  }
+}
+
+}  // namespace
+
+// lnmode: 0 = A is bf16; 1 = A = LN(X f32) with (g1,b1); 2 = A = LN(LN(X)) with (g1,b1) then (g2,b2).
+// epi: 0 = store act(acc+bias) as out_dtype; 1 = f32 Y += acc + bias; 2 = split-K partial products
+// (f32, no bias) for split s at Y + s*split_stride + row*ldy + n, K split over ksplit workgroups per
+// column tile -- reduced (with bias + residual + the next LayerNorm) by itts_residual_reduce_ln.
+// M > 32 runs ceil(M/32) row tiles.
+extern "C" int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed, int K, int N, int M,
+                                const float* bias, const float* g1, const float* b1, const float* g2, const float* b2,
+                                int lnmode, int gelu, int epi, void* y, int64_t ldy, int out_dtype,
+                                int64_t split_stride, int ksplit, void* stream) {
+  const char* fn = "itts_decode_gemm";
+  ITTS_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 16 == 0, fn, "bad sizes");
+  if (M == 0) return 0;
+  ITTS_REQUIRE(a && w_packed && y, fn, "null pointer");
+  ITTS_REQUIRE(lnmode == 0 || (g1 && b1 && (lnmode == 1 || (g2 && b2))), fn, "LayerNorm params missing");
+  ITTS_REQUIRE(lnmode == 0 || K == 1024 || K == 256 || K == 512, fn, "LN prologue supports K in {256, 512, 1024}");
+  ITTS_REQUIRE(epi >= 0 && epi <= 2, fn, "epi must be 0, 1 or 2");
+  ITTS_REQUIRE(epi == 0 || out_dtype == ITTS_F32, fn, "residual / partial epilogues are f32");
+  ITTS_REQUIRE(lnmode != 2 || epi == 0, fn, "double-LN prologue only with the store epilogue");
+  ITTS_REQUIRE(ksplit >= 1 && (K / 16) % ksplit == 0, fn, "K/16 must be a multiple of ksplit");
+  ITTS_REQUIRE(ksplit == 1 || epi == 2, fn, "ksplit > 1 requires epi 2");
+  ITTS_REQUIRE(epi != 2 || (lnmode == 0 && split_stride >= (int64_t)M * ldy), fn, "bad split-K partial layout");
+  DgArgs d{a, lda, static_cast<const u32x4_t*>(w_packed), K, N, M, bias, g1, b1, g2, b2, gelu, y, ldy, split_stride};
+  const int tiles = (M + 31) / 32;
+  hipStream_t s = itts::as_stream(stream);
+#define DG_LN(NWV, LNM, EPIV, OT)                                            \
+  do {                                                                       \
+    if (K == 1024) launch_dg<NWV, LNM, EPIV, 1024, OT>(d, tiles, 1, s);      \
+    else if (K == 512) launch_dg<NWV, LNM, EPIV, 512, OT>(d, tiles, 1, s);   \
+    else launch_dg<NWV, LNM, EPIV, 256, OT>(d, tiles, 1, s);                 \
+  } while (0)
+  if (lnmode == 0) {
+    if (epi == 2) {
+      launch_dg<8, 0, 2, 256, float>(d, tiles, ksplit, s);
+    } else if (epi == 1) {
+      launch_dg<8, 0, 1, 256, float>(d, tiles, 1, s);
+    } else if (out_dtype == ITTS_BF16) {
+      launch_dg<8, 0, 0, 256, uint16_t>(d, tiles, 1, s);
+    } else {
+      launch_dg<8, 0, 0, 256, float>(d, tiles, 1, s);
+    }
+  } else if (lnmode == 1) {
+    if (epi == 1) DG_LN(8, 1, 1, float);
+    else if (out_dtype == ITTS_BF16) DG_LN(8, 1, 0, uint16_t);
+    else DG_LN(8, 1, 0, float);
+  } else {
+    if (out_dtype == ITTS_BF16) DG_LN(8, 2, 0, uint16_t);
+    else DG_LN(8, 2, 0, float);
+  }
+#undef DG_LN
+  return itts::check_launch(fn);
+}

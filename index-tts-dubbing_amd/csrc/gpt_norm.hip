@@ -70,6 +70,66 @@ __global__ __launch_bounds__(kT) void ln_rows_kernel(const float* __restrict__ x
     if (i < n) St<TO>::st(yr + threadIdx.x + kT * i, v[i]);
 }
 
+// Decode-step variant: blockDim = D/4 threads, 4 consecutive elements (one float4) per thread, and
+// every load of the row (x, bias, all split partials) issued before the first use, so the kernel
+// pays one memory round trip instead of one per element group.
+constexpr int kMaxSplit = 8;
+
+__device__ __forceinline__ float block_sum_n(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+__device__ __forceinline__ void ln4(float (&v)[4], int D, const float* g, const float* b, float* red) {
+  const float mean = block_sum_n(v[0] + v[1] + v[2] + v[3], red) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q += (v[i] - mean) * (v[i] - mean);
+  const float rstd = rsqrtf(block_sum_n(q, red) / D + 1e-5f);
+  const f32x4_t g4 = *reinterpret_cast<const f32x4_t*>(g + 4 * threadIdx.x);
+  const f32x4_t b4 = *reinterpret_cast<const f32x4_t*>(b + 4 * threadIdx.x);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (v[i] - mean) * rstd * g4[i] + b4[i];
+}
+
+template <typename TO>
+__global__ __launch_bounds__(1024) void residual_reduce_ln_v4_kernel(
+    float* __restrict__ x, int64_t ldx, const float* __restrict__ part, int nsplit, int64_t split_stride, int64_t ldp,
+    const float* __restrict__ bias, TO* __restrict__ h, int64_t ldh, int D, const float* g1, const float* b1,
+    const float* g2, const float* b2) {
+  __shared__ float red[16];
+  const int m = blockIdx.x, e = 4 * threadIdx.x;
+  float* xr = x + (int64_t)m * ldx + e;
+  f32x4_t acc = *reinterpret_cast<const f32x4_t*>(xr);
+  f32x4_t pv[kMaxSplit];
+  f32x4_t bv = bias ? *reinterpret_cast<const f32x4_t*>(bias + e) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < kMaxSplit; ++s)
+    if (s < nsplit) pv[s] = *reinterpret_cast<const f32x4_t*>(part + s * split_stride + (int64_t)m * ldp + e);
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float p = bv[i];
+#pragma unroll
+    for (int s = 0; s < kMaxSplit; ++s)
+      if (s < nsplit) p += pv[s][i];
+    v[i] = acc[i] + p;
+  }
+  *reinterpret_cast<f32x4_t*>(xr) = f32x4_t{v[0], v[1], v[2], v[3]};
+  if (!g1) return;
+  ln4(v, D, g1, b1, red);
+  if (g2) ln4(v, D, g2, b2, red);
+  TO* hr = h + (int64_t)m * ldh + e;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) St<TO>::st(hr + i, v[i]);
+}
+
 template <typename TO>
 __global__ __launch_bounds__(kT) void residual_reduce_ln_kernel(float* __restrict__ x, int64_t ldx,
                                                                 const float* __restrict__ part, int nsplit,
@@ -129,6 +189,17 @@ extern "C" int itts_residual_reduce_ln(float* x, int64_t ldx, const float* part,
   if (M == 0) return 0;
   ITTS_REQUIRE(x && (nsplit == 0 || part) && (!g1 || (b1 && h)), fn, "null pointer");
   hipStream_t s = itts::as_stream(stream);
+  const bool v4 = D % 256 == 0 && D <= 4096 && nsplit <= kMaxSplit && ldx % 4 == 0 && ldp % 4 == 0 &&
+                  split_stride % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(part)) & 15) == 0;
+  if (v4) {
+    if (out_dtype == ITTS_BF16)
+      hipLaunchKernelGGL(residual_reduce_ln_v4_kernel<uint16_t>, dim3(M), dim3(D / 4), 0, s, x, ldx, part, nsplit,
+                         split_stride, ldp, bias, (uint16_t*)h, ldh, D, g1, b1, g2, b2);
+    else
+      hipLaunchKernelGGL(residual_reduce_ln_v4_kernel<float>, dim3(M), dim3(D / 4), 0, s, x, ldx, part, nsplit,
+                         split_stride, ldp, bias, (float*)h, ldh, D, g1, b1, g2, b2);
+    return itts::check_launch(fn);
+  }
   if (out_dtype == ITTS_BF16)
     hipLaunchKernelGGL(residual_reduce_ln_kernel<uint16_t>, dim3(M), dim3(kT), 0, s, x, ldx, part, nsplit,
                        split_stride, ldp, bias, (uint16_t*)h, ldh, D, g1, b1, g2, b2);

@@ -89,6 +89,7 @@ __global__ __launch_bounds__(kT) void sample_embed_kernel(const float* __restric
       x[(int64_t)b * D + e] = v[i];
       s += v[i];
     }
+  if (!h) return;  // bf16 decode path: the next GEMM normalises x in its own prologue
   // layer-0 ln_1
   s = wave_sum(s);
   __syncthreads();
@@ -126,7 +127,8 @@ extern "C" int itts_sample_embed(const float* logits, int64_t ldl, int V, uint8_
   ITTS_REQUIRE(B >= 0 && V > 0 && D > 0 && D <= kT * kMaxPer && (D % 64 == 0 || D < 64), fn, "bad sizes");
   if (B == 0) return 0;
   ITTS_REQUIRE(logits && seen && done && codes && tstate, fn, "null pointer");
-  ITTS_REQUIRE(!x || (emb && pos_emb && ln_g && ln_b && h), fn, "embedding output needs tables and ln_1");
+  ITTS_REQUIRE(!x || (emb && pos_emb), fn, "embedding output needs the embedding tables");
+  ITTS_REQUIRE(!h || (x && ln_g && ln_b), fn, "h output needs x and ln_1 params");
   hipStream_t s = itts::as_stream(stream);
   if (h_dtype == ITTS_BF16)
     hipLaunchKernelGGL(sample_embed_kernel<uint16_t>, dim3(B), dim3(kT), 0, s, logits, ldl, V, seen, done, codes, ldc,

@@ -42,8 +42,6 @@ SIGNATURES = {
     "itts_layernorm_rows": (_c_i, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp, _vp, _vp, _c_i, _vp]),
     "itts_residual_reduce_ln": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp,
                                        _vp, _vp, _c_i, _vp]),
-    "itts_skinny_gemm_bf16": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _c_i, _vp, _c_i64, _c_i, _vp, _c_i64,
-                                     _c_i, _vp]),
     "itts_gemm_f32": (_c_i, [_vp, _c_i64, _vp, _c_i64, _c_i, _c_i, _c_i, _vp, _c_i, _vp, _vp, _c_i64, _vp]),
     "itts_attn_decode": (_c_i, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_i, _vp, _c_i, _vp, _vp, _c_i64, _c_i, _c_i,
                                 _c_i, _c_i, _vp]),
@@ -52,6 +50,8 @@ SIGNATURES = {
     "itts_sample_embed": (_c_i, [_vp, _c_i64, _c_i, _vp, _vp, _vp, _c_i64, _vp, _c_i, _c_i, _c_i, _c_f, _vp, _vp, _c_i,
                                  _c_i, _vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp]),
     "itts_step_advance": (_c_i, [_vp, _c_i, _vp]),
+    "itts_decode_gemm": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _vp,
+                                _c_i64, _c_i, _c_i64, _c_i, _vp]),
 }
 
 _lib = None

@@ -125,9 +125,9 @@ class HipGPT:
         return emb, torch.tensor(pads, dtype=torch.int32, device=self.dev), s
 
     # ---------------- GEMM dispatch ----------------
-    def _gemm(self, A, w, Y=None, bias=None, gelu=False, residual=False, part=None, ksplit=1, skinny=False):
-        """Y = A @ W^T (+bias)(gelu)(+Y if residual); A [M, K].  skinny: decode-step weight-streaming
-        kernel (A rows padded to 32-row tiles; part = split-K f32 partials); else MFMA implicit GEMM."""
+    def _gemm(self, A, w, Y, bias=None, gelu=False, residual=False):
+        """Full-sequence GEMM Y = A @ W^T (+bias)(gelu)(+Y if residual), A [M, K]: the MFMA implicit
+        GEMM in bf16 mode, the exact-f32 GEMM in f32 mode (which also serves its decode step)."""
         M, K = A.shape
         N = w["N"]
         st = _hip.stream_ptr()
@@ -136,18 +136,10 @@ class HipGPT:
                                               _hip.ptr(bias), int(gelu), Y.data_ptr() if residual else None,
                                               Y.data_ptr(), Y.stride(0), st), "itts_gemm_f32")
             return
-        if not skinny:
-            _hip.check(self.lib.itts_igemm_fwd(A.data_ptr(), M * K, K, w["ig"].data_ptr(), _hip.ptr(bias), None,
-                                               Y.data_ptr() if residual else None, None, Y.data_ptr(), M * N,
-                                               Y.stride(0), None, 1, M, K, N, 1, _hip.i32_array([0]), 1, 0, 1.0,
-                                               int(gelu), _hip.dtype_code(Y), st), "itts_igemm_fwd")
-            return
-        assert not residual, "skinny path reduces residuals through itts_residual_reduce_ln"
-        _hip.check(self.lib.itts_skinny_gemm_bf16(
-            A.data_ptr(), A.stride(0), w["sk"].data_ptr(), K, N, M, _hip.ptr(bias) if part is None else None,
-            int(gelu), None if Y is None else Y.data_ptr(), 0 if Y is None else Y.stride(0),
-            BF16 if (Y is not None and Y.dtype == torch.bfloat16) else F32,
-            None if part is None else part.data_ptr(), N, ksplit, st), "itts_skinny_gemm_bf16")
+        _hip.check(self.lib.itts_igemm_fwd(A.data_ptr(), M * K, K, w["ig"].data_ptr(), _hip.ptr(bias), None,
+                                           Y.data_ptr() if residual else None, None, Y.data_ptr(), M * N,
+                                           Y.stride(0), None, 1, M, K, N, 1, _hip.i32_array([0]), 1, 0, 1.0,
+                                           int(gelu), _hip.dtype_code(Y), st), "itts_igemm_fwd")
 
     def _ln(self, x, y, ln, ln2=None, idx=None, M=None):
         M = x.shape[0] if M is None else M
@@ -202,7 +194,7 @@ class HipGPT:
             "qkv": torch.zeros(B, 3 * D, device=dev),
             "o": torch.zeros(Mp, D, dtype=ad, device=dev),
             "f": torch.zeros(Mp, 4 * D, dtype=ad, device=dev),
-            "part": torch.zeros(8, B, 4 * D, device=dev),
+            "ws": torch.zeros(8 * B * D, device=dev),  # split-K partial products [split][B][D]
             "logits": torch.zeros(B, self.V, device=dev),
             "kc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
             "vc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
@@ -227,10 +219,12 @@ class HipGPT:
         """One fed token per row -> next token sampled (all device-side; graph-capturable)."""
         B, D = st["B"], self.D
         stream = _hip.stream_ptr()
-        x, h, qkv, o, f, part = st["x"], st["h"], st["qkv"], st["o"], st["f"], st["part"]
-        hB = h[:B]
+        x, h, qkv, o, f = st["x"], st["h"], st["qkv"], st["o"], st["f"]
         for li, ly in enumerate(self.layers):
-            self._gemm(hB, ly.w["qkv"], qkv, bias=ly.b["qkv"], skinny=True)
+            if self.mode == "f32":
+                self._gemm(h[:B], ly.w["qkv"], qkv, bias=ly.b["qkv"])
+            else:  # h = ln_1(x) was produced by the previous reduce (or the sampler for layer 0)
+                self._dg(h, ly.w["qkv"], B, ly.b["qkv"], qkv)
             kc, vc = st["kc"][li], st["vc"][li]
             _hip.check(self.lib.itts_attn_decode(
                 qkv.data_ptr(), 3 * D, kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1), self.max_kv,
@@ -247,33 +241,52 @@ class HipGPT:
                 else:
                     self._ln(x, h, self.ln_f, self.final_norm, M=B)
                 continue
-            ko = self._ksplit(D)
-            self._gemm(o[:B], ly.w["o"], part=part, ksplit=ko, skinny=True)
+            ko = self._ksplit(ly.w["o"]["K"], self.KSPLIT["o"])
+            self._dg(o, ly.w["o"], B, None, st["ws"], epi=2, ksplit=ko)
             self._reduce(st, ko, ly.b["o"], ly.ln2)
-            self._gemm(h[:B], ly.w["fc"], f, bias=ly.b["fc"], gelu=True, skinny=True)
-            kp = self._ksplit(4 * D)
-            self._gemm(f[:B], ly.w["proj"], part=part, ksplit=kp, skinny=True)
+            self._dg(h, ly.w["fc"], B, ly.b["fc"], f, gelu=True)
+            kp = self._ksplit(ly.w["proj"]["K"], self.KSPLIT["proj"])
+            self._dg(f, ly.w["proj"], B, None, st["ws"], epi=2, ksplit=kp)
             if nxt is not None:
                 self._reduce(st, kp, ly.b["proj"], nxt)
             else:
                 self._reduce(st, kp, ly.b["proj"], self.ln_f, self.final_norm)
-        self._gemm(h[:B], self.head_w, st["logits"], bias=self.head_b, skinny=True)
+        if self.mode == "f32":
+            self._gemm(h[:B], self.head_w, st["logits"], bias=self.head_b)
+        else:
+            self._dg(h, self.head_w, B, self.head_b, st["logits"])
         self._sample(st, 1, min_new, penalty)
         _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
+    # split-K factors of the residual projections (partials reduced by itts_residual_reduce_ln)
+    KSPLIT = {"o": 2, "proj": 8}
+
     @staticmethod
-    def _ksplit(K):
-        ks = K // 16
-        for s in (8, 4, 2):
-            if ks % s == 0 and ks // s >= 8:
-                return s
-        return 1
+    def _ksplit(K, want):
+        ks = want
+        while ks > 1 and (K // 16) % ks:
+            ks //= 2
+        return ks
+
+    def _dg(self, A, w, M, bias, Y, ln=None, ln2=None, gelu=False, epi=0, ksplit=1):
+        """itts_decode_gemm: Y = act(prologue(A) @ W^T + bias) (epi 0), Y += ... (epi 1), or split-K
+        partial products into Y (epi 2); the prologue is identity (bf16 A) or the (double) LayerNorm of
+        the f32 residual stream A."""
+        mode = 0 if ln is None else (1 if ln2 is None else 2)
+        N = w["N"]
+        _hip.check(self.lib.itts_decode_gemm(
+            A.data_ptr(), A.stride(0), w["sk"].data_ptr(), w["K"], N, M, _hip.ptr(bias),
+            None if ln is None else ln[0].data_ptr(), None if ln is None else ln[1].data_ptr(),
+            None if ln2 is None else ln2[0].data_ptr(), None if ln2 is None else ln2[1].data_ptr(),
+            mode, int(gelu), epi, Y.data_ptr(), N if epi == 2 else Y.stride(0), _hip.dtype_code(Y),
+            M * N, ksplit, _hip.stream_ptr()), "itts_decode_gemm")
 
     def _reduce(self, st, nsplit, bias, ln, ln2=None):
+        """x += bias + sum of the split-K partials (fixed order); h = LN(x) (or LN2(LN(x)))."""
         B, D = st["B"], self.D
-        part, x, h = st["part"], st["x"], st["h"]
+        x, h = st["x"], st["h"]
         _hip.check(self.lib.itts_residual_reduce_ln(
-            x.data_ptr(), D, part.data_ptr(), nsplit, B * D, D, bias.data_ptr(), h.data_ptr(), D, B, D,
+            x.data_ptr(), D, st["ws"].data_ptr(), nsplit, B * D, D, bias.data_ptr(), h.data_ptr(), D, B, D,
             ln[0].data_ptr(), ln[1].data_ptr(), None if ln2 is None else ln2[0].data_ptr(),
             None if ln2 is None else ln2[1].data_ptr(), _hip.dtype_code(h), _hip.stream_ptr()),
             "itts_residual_reduce_ln")
@@ -321,7 +334,10 @@ class HipGPT:
         self._forward_rows(x, starts, lens, pad, s + 1, cache=(st["kc"], st["vc"]))
         last = (starts + s).contiguous()
         self._ln(x, st["h"], self.ln_f, self.final_norm, idx=last, M=B)
-        self._gemm(st["h"][:B], self.head_w, st["logits"], bias=self.head_b, skinny=True)
+        if self.mode == "f32":
+            self._gemm(st["h"][:B], self.head_w, st["logits"], bias=self.head_b)
+        else:
+            self._dg(st["h"], self.head_w, B, self.head_b, st["logits"])
         self._sample(st, 0, min_new_tokens, repetition_penalty)
         # ---- decode loop ----
         steps = 1

@@ -69,20 +69,39 @@ class BatchedTTS:
 
     @torch.no_grad()
     def synthesize(self, mels: Sequence[torch.Tensor], texts: Sequence[torch.Tensor], max_mel_tokens: int = 600,
-                   repetition_penalty: float = 10.0, min_new_tokens: int = 0, keys=None, use_graph: bool = True):
+                   repetition_penalty: float = 10.0, min_new_tokens: int = 0, keys=None, use_graph: bool = True,
+                   timings: Optional[dict] = None):
         """mels[b]: prompt log-mel [1, 100, T_b]; texts[b]: token ids [L_b].
-        -> (pcm int16 [B, Tmax] on device, sample lengths [B] (cpu), codes list)."""
+        -> (pcm int16 [B, Tmax] on device, sample lengths [B] (cpu), codes list).
+        ``timings``: if a dict is given, per-phase wall seconds are accumulated into it (adds syncs)."""
+        import time
+
+        def mark(name, t=[None]):
+            if timings is None:
+                return
+            torch.cuda.synchronize(self.device)
+            now = time.perf_counter()
+            if t[0] is not None:
+                timings[name] = timings.get(name, 0.0) + now - t[0]
+            t[0] = now
+
+        mark(None)
         B = len(texts)
         conds, spk = self.prompt_features(mels, keys)
+        mark("prompt_features")
         L = max(int(t.numel()) for t in texts)
         ids = torch.full((B, L), self.stop_text, dtype=torch.long)
         for b, t in enumerate(texts):
             ids[b, : t.numel()] = t.reshape(-1).long()
         codes = self.gpt.generate(conds, ids.to(self.device), max_mel_tokens, repetition_penalty=repetition_penalty,
                                   min_new_tokens=min_new_tokens, use_graph=use_graph)
+        mark("gpt_generate")
         rows = codes.cpu().numpy()
         fixed = [torch.from_numpy(remove_long_silence(rows[b], self.stop)) for b in range(B)]
         fixed = [f if f.numel() > 0 else torch.tensor([self.stop]) for f in fixed]  # degenerate: nothing generated
+        mark("remove_long_silence")
         latent, lens = self.gpt.latent(conds, [t.reshape(-1) for t in texts], fixed)
+        mark("latent_pass")
         _, pcm = self.vocoder.forward(latent, lens, spk)
+        mark("vocoder")
         return pcm, (lens.long() * HOP), fixed

@@ -1,0 +1,98 @@
+"""GPU unit tests of individual GPT kernels through the C ABI vs. plain PyTorch fp32 references.
+
+Tolerance: bf16 GEMM operands (the reference uses the same bf16-rounded operands) with f32
+accumulation -> |err| <= 1e-2 * (|A| @ |W|^T) (+ bf16 output rounding for bf16 outputs)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from indextts import _hip
+    return _hip, _hip.load()
+
+
+@pytest.mark.parametrize("K,N,M", [(256, 96, 3), (256, 256, 1), (512, 512, 1), (1024, 3072, 32), (1024, 8194, 32),
+                                   (4096, 1024, 32), (1024, 1024, 45)])
+@pytest.mark.parametrize("mode", ["plain", "ln", "ln2", "resid", "split2", "split8", "gelu_bf16"])
+def test_decode_gemm(K, N, M, mode):
+    from indextts.gpt.engine import pack_skinny
+    _hip, lib = _lib()
+    if mode in ("ln", "ln2") and K > 1024:
+        pytest.skip("LN prologue is for K <= 1024")
+    ksplit = int(mode[-1]) if mode.startswith("split") else 1
+    if ksplit > 1 and (K // 16) % ksplit:
+        pytest.skip("K/16 not divisible by ksplit")
+    torch.manual_seed(K + N + M)
+    Mp = (M + 31) // 32 * 32
+    W = torch.randn(N, K) / K ** 0.5
+    bias = torch.randn(N) * 0.1
+    wsk = pack_skinny(W).cuda()
+    g1, b1 = torch.randn(K) * 0.1 + 1, torch.randn(K) * 0.1
+    g2, b2 = torch.randn(K) * 0.1 + 1, torch.randn(K) * 0.1
+    X = torch.randn(Mp, K) * 2 + 0.5
+    Wq = W.to(torch.bfloat16).float()
+    lnm = {"ln": 1, "ln2": 2}.get(mode, 0)
+    if lnm:
+        A = F.layer_norm(X[:M], (K,), g1, b1, 1e-5)
+        if lnm == 2:
+            A = F.layer_norm(A, (K,), g2, b2, 1e-5)
+        a_dev = X.cuda()
+    else:
+        A = X[:M].to(torch.bfloat16).float()
+        a_dev = X.to(torch.bfloat16).cuda()
+    prod = A.to(torch.bfloat16).float() @ Wq.t()
+    gelu = mode == "gelu_bf16"
+    epi = 2 if ksplit > 1 else (1 if mode == "resid" else 0)
+    Y0 = torch.randn(Mp, N)
+    if epi == 2:
+        Y = torch.zeros(ksplit, M, N).cuda()
+        ref = prod
+    else:
+        ref = prod + bias
+        if gelu:
+            ref = F.gelu(ref, approximate="tanh")
+        if epi == 1:
+            ref = ref + Y0[:M]
+        Y = Y0.clone().to(torch.bfloat16 if gelu else torch.float32).cuda()
+    gd, bd, g2d, b2d = g1.cuda(), b1.cuda(), g2.cuda(), b2.cuda()
+    biasd = bias.cuda()
+    _hip.check(lib.itts_decode_gemm(a_dev.data_ptr(), K, wsk.data_ptr(), K, N, M,
+                                    None if epi == 2 else biasd.data_ptr(),
+                                    gd.data_ptr() if lnm else None, bd.data_ptr() if lnm else None,
+                                    g2d.data_ptr() if lnm == 2 else None, b2d.data_ptr() if lnm == 2 else None,
+                                    lnm, int(gelu), epi, Y.data_ptr(), N, _hip.dtype_code(Y), M * N, ksplit,
+                                    _hip.stream_ptr()), "decode_gemm")
+    torch.cuda.synchronize()
+    got = Y.sum(0).cpu() if epi == 2 else Y[:M].float().cpu()
+    assert torch.isfinite(got).all()
+    scale = (A.abs() @ Wq.abs().t()) + 1e-3
+    tol = (2e-2 if gelu else 1e-2) * scale + (1e-2 if gelu else 0)
+    err = (got - ref).abs()
+    assert bool((err <= tol).all()), float((err / scale).max())
+    if epi != 2 and Mp > M:  # rows beyond M untouched
+        assert torch.equal(Y[M:].float().cpu(), Y0[M:].to(Y.dtype).float())
+
+
+def test_residual_reduce_ln_matches_torch():
+    _hip, lib = _lib()
+    torch.manual_seed(0)
+    B, D, S = 32, 1024, 8
+    x = torch.randn(B, D)
+    part = torch.randn(S, B, D)
+    bias = torch.randn(D)
+    g1, b1, g2, b2 = torch.randn(D) + 1, torch.randn(D), torch.randn(D) + 1, torch.randn(D)
+    xd, pd = x.clone().cuda(), part.cuda()
+    h = torch.zeros(B, D, dtype=torch.bfloat16).cuda()
+    args = [t.cuda() for t in (bias, g1, b1, g2, b2)]
+    _hip.check(lib.itts_residual_reduce_ln(xd.data_ptr(), D, pd.data_ptr(), S, B * D, D, args[0].data_ptr(),
+                                           h.data_ptr(), D, B, D, args[1].data_ptr(), args[2].data_ptr(),
+                                           args[3].data_ptr(), args[4].data_ptr(), _hip.BF16, _hip.stream_ptr()),
+               "reduce")
+    torch.cuda.synchronize()
+    xr = x + bias + part.sum(0)
+    hr = F.layer_norm(F.layer_norm(xr, (D,), g1, b1, 1e-5), (D,), g2, b2, 1e-5)
+    torch.testing.assert_close(xd.cpu(), xr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(h.float().cpu(), hr, rtol=1e-2, atol=2e-2)
