@@ -1,0 +1,132 @@
+/* libitts_hip.so -- C ABI of the MI355X (gfx950) IndexTTS hot path:
+ *   GPT speech-token decode (reference indextts/gpt/model.py + HF GPT-2) and the BigVGAN2 vocoder
+ *   (reference indextts/BigVGAN/).
+ *
+ * Conventions (all entry points):
+ *   - plain pointers to DEVICE memory allocated by the caller (the library never allocates or
+ *     frees on the hot path); sizes / strides in elements; `stream` is a hipStream_t (NULL = the
+ *     legacy default stream); launches are asynchronous, no host synchronisation;
+ *   - return 0 on success, nonzero on an argument error or a HIP launch error; the message is in
+ *     itts_last_error() (thread-local); no C++ exception crosses the ABI;
+ *   - dtype codes: ITTS_F32 = 0, ITTS_BF16 = 1;
+ *   - "channel-last" vocoder activations are [B][T][C] with per-sequence lengths[B] (ragged batch):
+ *     rows t >= lengths[b] are never read as data (edge handling equals the reference's padding);
+ *   - callable from any host thread; ctypes releases the GIL around every call.
+ *
+ * The reference's only native boundary on this path is the fused anti-alias activation extension
+ * (anti_alias_activation_cuda.forward, BigVGAN/alias_free_activation/cuda/anti_alias_activation.cpp:19-23,
+ * anti_alias_activation_cuda.cu:214-256); everything else in the reference is PyTorch / HF
+ * transformers modules.  Each function below cites the reference code it replaces.
+ */
+#ifndef ITTS_HIP_H_
+#define ITTS_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ITTS_DTYPE_F32 = 0, ITTS_DTYPE_BF16 = 1 };
+
+/* ---- runtime -------------------------------------------------------------------------------- */
+const char* itts_last_error(void);
+int itts_abi_version(void);
+const char* itts_build_target(void); /* "gfx950" */
+
+/* ---- BigVGAN2 vocoder ----------------------------------------------------------------------- */
+
+/* Fused Activation1d(SnakeBeta): 2x upsample (replicate pad 5/5, 12-tap kaiser-sinc transposed conv,
+ * crop 15/15) -> x + 1/(exp(beta)+1e-9) * sin^2(x*exp(alpha)) -> 2x downsample (replicate pad 5/6,
+ * 12-tap lowpass, stride 2).  Replaces anti_alias_activation_cuda.forward
+ * (anti_alias_activation_cuda.cu:214-256) and its torch path Activation1d.forward
+ * (alias_free_torch/act.py:24-29, resample.py:25-49, filter.py:87-96, activations.py:109-122);
+ * the parity target is the torch path (quirk Q7: the CUDA kernel differs on the first/last 3 samples).
+ * Arbitrary strides (x_sb/x_st/x_sc = batch/time/channel strides); lengths may be NULL (all T). */
+int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, const float* down12, const float* log_alpha,
+                          const float* log_beta, const int32_t* lengths, int B, int C, int T, int64_t x_sb,
+                          int64_t x_st, int64_t x_sc, int64_t y_sb, int64_t y_st, int64_t y_sc, int dtype_in,
+                          int dtype_out, void* stream);
+/* Same, for contiguous [B][C][T] tensors -- exactly the reference extension's argument list
+ * (input, up_filter, down_filter, alpha, beta; anti_alias_activation.cpp:19-23), caller-owned output. */
+int itts_aa_snakebeta_bct(const void* x, void* y, const float* up12, const float* down12, const float* log_alpha,
+                          const float* log_beta, int B, int C, int T, int dtype, void* stream);
+
+/* Padded channel counts of the packed conv weights (K chunk of 32/64, N tile of 32/128). */
+int itts_igemm_pack_dims(int Cin, int Cout, int* ci_pad, int* co_pad);
+/* Implicit-GEMM 1-D convolution on MFMA (bf16 operands, f32 accumulate), channel-last, ragged:
+ *   y[b][t*y_row_mul + y_row_off][:] = alpha * (act(sum_k x[b][t + tap_off[k]][:] @ W_k + bias + bias_b[b]) + r1 + r2)
+ * with zero padding outside [0, lengths[b]).  Covers every Conv1d of the generator (conv_pre,
+ * AMPBlock1 dilated convs with the residual add and the /num_kernels average fused in,
+ * models.py:65-74,224-243), the polyphase ConvTranspose1d upsamplers (models.py:155-161,228-231)
+ * and the GPT sequence GEMMs (HF Conv1D, pytorch_utils.py:119, as 1-tap convolutions).
+ * tap_off is a HOST array of ntaps offsets. */
+int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, const float* bias,
+                   const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy,
+                   const int32_t* lengths, int B, int Tmax, int Cin, int Cout, int ntaps, const int32_t* tap_off,
+                   int y_row_mul, int y_row_off, float alpha, int gelu, int out_dtype, void* stream);
+/* conv_post (Conv1d(C->1, K, pad K/2), bias) + tanh (models.py:246-248), optionally also the int16
+ * PCM of infer.py:627,653 (clamp(32767*wav, +-32767) truncated toward zero, quirk Q8). */
+int itts_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* w, float bias, int C, int K,
+                        const int32_t* lengths, int B, int Tmax, float* wav, int16_t* pcm, int64_t y_sb,
+                        int dtype_in, void* stream);
+
+/* ---- GPT (UnifiedVoice + HF GPT-2) ------------------------------------------------------------ */
+
+/* y[r] = LN2(LN1(x[row_idx ? row_idx[r] : r])) (LN2 optional; eps 1e-5).  ln_1 / ln_2 / ln_f and
+ * the double norm before mel_head (HF modeling_gpt2.py:620 ln_f, gpt/model.py:48 final_norm; Q5). */
+int itts_layernorm_rows(const float* x, int64_t ldx, const int32_t* row_idx, void* y, int64_t ldy, int M, int D,
+                        const float* g1, const float* b1, const float* g2, const float* b2, int out_dtype,
+                        void* stream);
+/* x[m] += bias + sum_s part[s][m] (fixed order), then h[m] = LN2(LN1(x[m])): the residual add of
+ * attn.c_proj / mlp.c_proj (HF modeling_gpt2.py:246-306) fused with the next LayerNorm. */
+int itts_residual_reduce_ln(float* x, int64_t ldx, const float* part, int nsplit, int64_t split_stride, int64_t ldp,
+                            const float* bias, void* h, int64_t ldh, int M, int D, const float* g1, const float* b1,
+                            const float* g2, const float* b2, int out_dtype, void* stream);
+/* Exact-f32 GEMM (one fmaf chain per output in k order): the f32 verification mode of every GPT
+ * linear layer (HF Conv1D). */
+int itts_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, int M, int N, int K, const float* bias,
+                  int gelu, const float* r1, float* Y, int64_t ldy, void* stream);
+/* Decode-step GEMM for M <= 32 rows on MFMA with weights prepacked in fragment order; epi 0:
+ * y = act(acc + bias), 1: y += acc + bias, 2: split-K partials y[ks][m][n] (reduced by
+ * itts_residual_reduce_ln).  lnmode 1/2 normalises f32 rows of `a` in the prologue.  c_attn / c_proj /
+ * c_fc / mlp.c_proj and mel_head of the KV-cached decode (gpt/model.py:85-192, HF :185-243). */
+int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed, int K, int N, int M, const float* bias,
+                     const float* g1, const float* b1, const float* g2, const float* b2, int lnmode, int gelu, int epi,
+                     void* y, int64_t ldy, int out_dtype, int64_t split_stride, int ksplit, void* stream);
+/* One decode step of 16x64 causal attention per row: appends this step's k/v at position
+ * kv_base + tstate[0] of the cache [B][H][smax][64] and attends over the valid (pad-masked,
+ * quirk Q2) prefix.  HF modeling_gpt2.py:54-72,185-225 with the additive padding mask. */
+int itts_attn_decode(const float* qkv, int64_t ldqkv, void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs,
+                     int smax, const int32_t* pad, int kv_base, const int32_t* tstate, void* out, int64_t ldo, int B,
+                     int H, int cache_dtype, int out_dtype, void* stream);
+/* Causal attention over packed variable-length sequences (prefill and latent pass); optionally
+ * writes K/V into the decode cache.  seq_pad[b] leading rows are masked (left padding, Q2). */
+int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start, const int32_t* seq_len,
+                      const int32_t* seq_pad, int nseq, int max_len, void* cache_k, void* cache_v, int64_t cache_bs,
+                      int64_t cache_hs, void* out, int64_t ldo, int H, int cache_dtype, int out_dtype, void* stream);
+/* Greedy token selection + next-token embedding, per row:
+ * RepetitionPenalty over all seen ids incl. the fake prefix ids (Q4; HF logits_process.py:409-412),
+ * min_new_tokens, first-index argmax (HF generation/utils.py:2894-2925), finished rows -> stop,
+ * x = mel_embedding(tok) + mel_pos[col + pos_delta] (Q1, gpt/model.py:151-155), h = ln_1(x).
+ * col = tstate[0] + col_delta (device counter: graph-replayable).  forced (tests): feed these ids. */
+int itts_sample_embed(const float* logits, int64_t ldl, int V, uint8_t* seen, uint8_t* done, int32_t* codes,
+                      int64_t ldc, const int32_t* tstate, int col_delta, int min_new, int stop, float penalty,
+                      const float* emb, const float* pos_emb, int pos_delta, int D, const float* ln_g,
+                      const float* ln_b, float* x, void* h, int h_dtype, int B, const int32_t* forced, void* stream);
+/* do_sample=True variant: Temperature -> TopK (1..64, ties at the k-th value kept) -> TopP warpers
+ * and a multinomial draw (HF 4.36 `sample`; infer.py:535-543 defaults top_k 30 / top_p 0.8).
+ * top_k == 0 (with top_p == 1): draw from the full softmax.  RNG: counter hash of
+ * (seed = tstate[2] | tstate[3] << 32, row, column) -- statistical parity with torch.multinomial. */
+int itts_sample_topk_embed(const float* logits, int64_t ldl, int V, uint8_t* seen, uint8_t* done, int32_t* codes,
+                           int64_t ldc, const int32_t* tstate, int col_delta, int min_new, int stop, float penalty,
+                           float temperature, int top_k, float top_p, const float* emb, const float* pos_emb,
+                           int pos_delta, int D, const float* ln_g, const float* ln_b, float* x, void* h,
+                           int h_dtype, int B, const int32_t* forced, void* stream);
+/* tstate[0] += delta on the device (advances the decode column between graph replays). */
+int itts_step_advance(int32_t* tstate, int delta, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ITTS_HIP_H_ */

@@ -5,6 +5,8 @@
 
 #include <string>
 
+#include "itts_hip.h"  // the public C ABI: definitions below must match these declarations
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;

@@ -49,6 +49,8 @@ SIGNATURES = {
                                  _c_i, _c_i, _vp]),
     "itts_sample_embed": (_c_i, [_vp, _c_i64, _c_i, _vp, _vp, _vp, _c_i64, _vp, _c_i, _c_i, _c_i, _c_f, _vp, _vp, _c_i,
                                  _c_i, _vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp]),
+    "itts_sample_topk_embed": (_c_i, [_vp, _c_i64, _c_i, _vp, _vp, _vp, _c_i64, _vp, _c_i, _c_i, _c_i, _c_f, _c_f,
+                                      _c_i, _c_f, _vp, _vp, _c_i, _c_i, _vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp]),
     "itts_step_advance": (_c_i, [_vp, _c_i, _vp]),
     "itts_decode_gemm": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _vp,
                                 _c_i64, _c_i, _c_i64, _c_i, _vp]),

@@ -207,6 +207,16 @@ class HipGPT:
         return st
 
     def _sample(self, st, col_delta, min_new, penalty):
+        smp = st.get("sampling")
+        if smp is not None:  # (temperature, top_k, top_p); the seed is device state (t[2:4])
+            _hip.check(self.lib.itts_sample_topk_embed(
+                st["logits"].data_ptr(), self.V, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
+                st["codes"].data_ptr(), st["max_new"], st["t"].data_ptr(), col_delta, int(min_new), self.stop_mel,
+                float(penalty), float(smp[0]), int(smp[1]), float(smp[2]), self.mel_emb.data_ptr(),
+                self.mel_pos.data_ptr(), 2, self.D, self.layers[0].ln1[0].data_ptr(), self.layers[0].ln1[1].data_ptr(),
+                st["x"].data_ptr(), st["h"].data_ptr(), _hip.dtype_code(st["h"]), st["B"],
+                _hip.ptr(st.get("forced")), _hip.stream_ptr()), "itts_sample_topk_embed")
+            return
         _hip.check(self.lib.itts_sample_embed(
             st["logits"].data_ptr(), self.V, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
             st["codes"].data_ptr(), st["max_new"], st["t"].data_ptr(), col_delta, int(min_new), self.stop_mel,
@@ -295,9 +305,13 @@ class HipGPT:
     @torch.no_grad()
     def generate(self, conds: torch.Tensor, text_ids: torch.Tensor, max_new_tokens: int,
                  repetition_penalty: float = 10.0, min_new_tokens: int = 0, use_graph: bool = True,
-                 check_every: int = 16, forced_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Greedy decode (do_sample=False, num_beams=1) -> codes [B, n] int64 on the device, finished
-        rows padded with the stop token, n = steps until every row stopped (or max_new_tokens)."""
+                 check_every: int = 16, forced_codes: Optional[torch.Tensor] = None, do_sample: bool = False,
+                 temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
+                 seed: Optional[int] = None) -> torch.Tensor:
+        """Greedy (do_sample=False) or top-k/top-p sampling (do_sample=True; num_beams=1) decode
+        -> codes [B, n] int64 on the device, finished rows padded with the stop token, n = steps until
+        every row stopped (or max_new_tokens).  ``seed`` (default: drawn from torch's CPU generator)
+        keys the device RNG, so a fixed seed reproduces the draws."""
         emb, pad, s = self.prepare_inputs(conds, text_ids)
         B = emb.shape[0]
         assert s + 1 + max_new_tokens <= self.max_kv, "KV capacity exceeded"
@@ -315,6 +329,15 @@ class HipGPT:
         st["done"].zero_()
         st["t"].zero_()
         st["codes"].fill_(self.stop_mel)
+        st["sampling"] = (float(temperature), int(top_k), float(top_p)) if do_sample else None
+        if do_sample:
+            if seed is None:
+                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            seed &= (1 << 64) - 1
+            lo, hi = seed & 0xFFFFFFFF, seed >> 32
+            st["t"][2:4].copy_(torch.tensor([lo - (1 << 32) if lo >= 1 << 31 else lo,
+                                             hi - (1 << 32) if hi >= 1 << 31 else hi], dtype=torch.int32))
+        gkey = (min_new_tokens, repetition_penalty, st["sampling"])
         if forced_codes is not None:  # teacher forcing (tests): feed these ids, record the argmax ids
             fc = torch.full((B, max_new_tokens), self.stop_mel, dtype=torch.int32, device=self.dev)
             fc[:, : forced_codes.shape[1]] = forced_codes.to(self.dev, torch.int32)
@@ -341,9 +364,10 @@ class HipGPT:
         self._sample(st, 0, min_new_tokens, repetition_penalty)
         # ---- decode loop ----
         steps = 1
-        graph_ok = use_graph and self._graph is not None and self._graph[1] == (min_new_tokens, repetition_penalty)
+        graph_ok = use_graph and self._graph is not None and self._graph[1] == gkey
         if use_graph and not graph_ok and max_new_tokens > 1:
             self._capture(st, min_new_tokens, repetition_penalty)
+            self._graph = (self._graph[0], gkey)
             graph_ok = True
         while steps < max_new_tokens:
             if graph_ok:

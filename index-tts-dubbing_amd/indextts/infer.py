@@ -1,0 +1,306 @@
+"""Drop-in ``indextts.infer.IndexTTS`` (reference ``indextts/infer.py:26-660``) on the HIP path.
+
+Same constructor, methods, argument meaning, return values and attributes as the reference, so the
+reference's callers (``indextts/cli.py``, ``webui.py``, ``srt_dubbing``'s
+``IndexTTSEngine``, which introspects ``inspect.signature(IndexTTS.infer)``, quirk Q9) run unchanged.
+What differs is underneath:
+
+* every sentence of one ``infer`` / ``infer_fast`` call is synthesised in ONE batched pass
+  (``pipeline.BatchedTTS``: batched GPT prefill + hipGraph decode, batched latent pass, ragged
+  batched vocoder) instead of a Python loop over sentences; per-sentence results are unchanged
+  because every kernel is row-independent (tests/test_gpu_gpt.py batch-invariance tests);
+* ``is_fp16=True`` computes in bf16 (MFMA) with f32 accumulation / residual stream / logits;
+  ``is_fp16=False`` runs the exact-f32 verification kernels;
+* there is no CPU / MPS path and no silent fallback: without a GPU or without ``libitts_hip.so``
+  the constructor raises (the reference fell back to torch, infer.py:97-109);
+* decoding: greedy (``do_sample=False, num_beams=1``) reproduces the reference's ids exactly (f32);
+  ``do_sample=True`` runs the Temperature/TopK/TopP warpers + multinomial draw on the GPU with a
+  device RNG (same distribution, different draws than torch -- statistical parity).  Beam search
+  (``num_beams > 1``, the reference default) is not implemented yet: it is decoded with
+  ``num_beams=1`` and a RuntimeWarning.  An extra ``seed=`` generation
+  kwarg fixes the device RNG.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+import warnings
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .pipeline import HOP, SR, BatchedTTS, remove_long_silence as _rls_row
+from .utils.audio import prompt_mel, save_wav_int16
+from .utils.config import load_config
+from .utils.text import TextNormalizer, TextTokenizer
+
+
+def _load_state_dict(path: str, key: Optional[str] = None) -> Dict[str, torch.Tensor]:
+    """torch.load with ``weights_only=True`` (never unpickles code); unwraps ``{"model": ...}``
+    (utils/checkpoint.py:25-27) or the given key (``"generator"`` for BigVGAN, infer.py:112-113)."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if key is not None:
+        sd = sd[key]
+    elif isinstance(sd, dict) and "model" in sd and isinstance(sd["model"], dict):
+        sd = sd["model"]
+    return sd
+
+
+class IndexTTS:
+    MAX_BATCH = 32
+
+    def __init__(self, cfg_path="checkpoints/config.yaml", model_dir="checkpoints", is_fp16=True, device=None,
+                 use_cuda_kernel=None):
+        if device is None:
+            if not torch.cuda.is_available():
+                raise RuntimeError("IndexTTS (MI355X build) needs a ROCm GPU; there is no CPU/MPS path")
+            device = "cuda:0"
+        if not str(device).startswith("cuda"):
+            raise RuntimeError(f"device {device!r}: the MI355X build runs on HIP devices ('cuda[:n]') only")
+        self.device = str(device)
+        self.is_fp16 = bool(is_fp16)
+        # the fused anti-alias activation is always the HIP kernel here; kept for API compatibility
+        self.use_cuda_kernel = use_cuda_kernel is None or bool(use_cuda_kernel)
+        self.cfg = load_config(cfg_path)
+        self.model_dir = model_dir
+        self.dtype = torch.bfloat16 if self.is_fp16 else None
+        self.stop_mel_token = self.cfg.gpt.stop_mel_token
+
+        self.gpt_path = os.path.join(model_dir, self.cfg.gpt_checkpoint)
+        self.bigvgan_path = os.path.join(model_dir, self.cfg.bigvgan_checkpoint)
+        gpt_sd = _load_state_dict(self.gpt_path)
+        print(">> GPT weights restored from:", self.gpt_path)
+        bv_sd = _load_state_dict(self.bigvgan_path, "generator")
+        print(">> bigvgan weights restored from:", self.bigvgan_path)
+        self.engine = BatchedTTS(gpt_sd, bv_sd, self.cfg, self.device, dtype="bf16" if self.is_fp16 else "f32")
+        self.gpt, self.bigvgan = self.engine.gpt, self.engine.vocoder
+        del gpt_sd, bv_sd
+
+        self.bpe_path = os.path.join(model_dir, self.cfg.dataset["bpe_model"])
+        self.normalizer = TextNormalizer()
+        self.normalizer.load()
+        print(">> TextNormalizer loaded")
+        self.tokenizer = TextTokenizer(self.bpe_path, self.normalizer)
+        print(">> bpe model loaded from:", self.bpe_path)
+        self.cache_audio_prompt = None
+        self.cache_cond_mel = None
+        self.gr_progress = None
+        self.model_version = self.cfg.version if "version" in self.cfg else None
+
+    # ------------------------------------------------------------------ host helpers (reference API)
+    def remove_long_silence(self, codes: torch.Tensor, silent_token=52, max_consecutive=30):
+        """infer.py:132-186: cut each row at its first stop token; rows with > max_consecutive silent
+        tokens keep at most 10 consecutive ones.  -> (codes [B, n], code_lens [B])"""
+        rows, lens, fixed = [], [], False
+        arr = codes.detach().cpu().numpy()
+        for r in arr:
+            kept = _rls_row(r, int(self.stop_mel_token), silent_token, max_consecutive)
+            hit = np.nonzero(r == self.stop_mel_token)[0]
+            n_cut = int(hit[0]) if len(hit) else r.shape[0]
+            if int((r == silent_token).sum()) > max_consecutive:
+                fixed = True
+            rows.append(kept)
+            lens.append(kept.shape[0] if int((r == silent_token).sum()) > max_consecutive else n_cut)
+        if fixed:
+            width = max(x.shape[0] for x in rows)
+            out = np.full((len(rows), width), self.stop_mel_token, dtype=arr.dtype)
+            for i, x in enumerate(rows):
+                out[i, : x.shape[0]] = x
+            codes = torch.from_numpy(out).to(codes.device)
+        mx = max(lens)
+        if mx < codes.shape[1]:
+            codes = codes[:, :mx]
+        return codes, torch.tensor(lens, dtype=torch.long, device=codes.device)
+
+    def bucket_sentences(self, sentences, bucket_max_size=4) -> List[List[Dict]]:
+        """infer.py:188-243: sort by length, open a new bucket when a sentence reaches 1.5x the running
+        bucket median or the bucket is full, then fold singleton buckets into open buckets."""
+        items = [{"idx": i, "sent": s, "len": len(s)} for i, s in enumerate(sentences)]
+        if len(items) <= bucket_max_size:
+            return [items]
+        buckets: List[List[Dict]] = []
+        median = 0
+        for it in sorted(items, key=lambda d: d["len"]):
+            if it["len"] == 0:
+                print(">> skip empty sentence")
+                continue
+            if not buckets or it["len"] >= int(median * 1.5) or len(buckets[-1]) >= bucket_max_size:
+                buckets.append([it])
+                median = it["len"]
+            else:
+                buckets[-1].append(it)
+                median = buckets[-1][len(buckets[-1]) // 2]["len"]
+        multi = [b for b in buckets if len(b) > 1]
+        singles = [b[0] for b in buckets if len(b) == 1]
+        for b in multi:
+            if not singles:
+                break
+            if len(b) < bucket_max_size:
+                b.append(singles.pop(0))
+        multi.extend(singles[i: i + bucket_max_size] for i in range(0, len(singles), bucket_max_size))
+        return multi
+
+    def pad_tokens_cat(self, tokens: List[torch.Tensor]) -> torch.Tensor:
+        """infer.py:245-262: v1.5+ right-pads [1, n] rows with stop_text; older versions pad up to 8
+        stop_text then start_text."""
+        width = max(t.shape[-1] for t in tokens)
+        stop, start = self.cfg.gpt.stop_text_token, self.cfg.gpt.start_text_token
+        out = torch.empty(len(tokens), width, dtype=tokens[0].dtype, device=tokens[0].device)
+        for i, t in enumerate(tokens):
+            row = t.reshape(-1)
+            n = row.numel()
+            out[i, :n] = row
+            if self.model_version and self.model_version >= 1.5:
+                out[i, n:] = stop
+            else:
+                k = min(8, width - n)
+                out[i, n: n + k] = stop
+                out[i, n + k:] = start
+        return out
+
+    def torch_empty_cache(self):
+        try:
+            torch.cuda.empty_cache()
+        except Exception:
+            pass
+
+    def _set_gr_progress(self, value, desc):
+        if self.gr_progress is not None:
+            self.gr_progress(value, desc=desc)
+
+    # ------------------------------------------------------------------ shared driver
+    def _prompt(self, audio_prompt):
+        if self.cache_cond_mel is None or self.cache_audio_prompt != audio_prompt:
+            cond_mel = prompt_mel(audio_prompt).to(self.device)
+            self.cache_audio_prompt = audio_prompt
+            self.cache_cond_mel = cond_mel
+            self.engine._prompt_cache.clear()  # conditioning / speaker embedding follow the mel cache
+        return self.cache_cond_mel
+
+    @staticmethod
+    def _decoding(kw: dict, max_tok_default=600):
+        do_sample = kw.pop("do_sample", True)
+        top_p = kw.pop("top_p", 0.8)
+        top_k = kw.pop("top_k", 30)
+        temperature = kw.pop("temperature", 1.0)
+        kw.pop("length_penalty", 0.0)  # only meaningful for beam search
+        num_beams = kw.pop("num_beams", 3)
+        repetition_penalty = kw.pop("repetition_penalty", 10.0)
+        max_mel_tokens = kw.pop("max_mel_tokens", max_tok_default)
+        min_new_tokens = kw.pop("min_new_tokens", 0)
+        seed = kw.pop("seed", None)
+        kw.pop("num_return_sequences", None)
+        if kw:
+            warnings.warn(f"ignored generation kwargs: {sorted(kw)}", RuntimeWarning)
+        if num_beams and num_beams > 1:
+            warnings.warn(f"num_beams={num_beams}: beam search is not implemented on the HIP path yet; "
+                          "decoding with num_beams=1", RuntimeWarning)
+        smp = {}
+        if do_sample:
+            top_k = int(top_k or 0)
+            if top_k > 64 or (top_k == 0 and top_p is not None and top_p < 1.0):
+                raise ValueError("HIP sampler supports 1 <= top_k <= 64 (or top_k=0 with top_p=1)")
+            smp = dict(do_sample=True, temperature=float(temperature), top_k=top_k,
+                       top_p=1.0 if top_p is None else float(top_p), seed=seed)
+        return dict(max_mel_tokens=int(max_mel_tokens), repetition_penalty=float(repetition_penalty),
+                    min_new_tokens=int(min_new_tokens), **smp)
+
+    def _run(self, cond_mel, sent_ids: List[torch.Tensor], dec: dict, groups=None):
+        """all sentences (chunks of MAX_BATCH) through the batched HIP pipeline -> (pcm rows, codes)."""
+        pcm_rows, codes_all = [], []
+        keys = [("prompt", self.cache_audio_prompt)]
+        B = self.MAX_BATCH
+        for c0 in range(0, len(sent_ids), B):
+            chunk = sent_ids[c0: c0 + B]
+            g = None
+            if groups is not None:  # groups never straddle a chunk boundary (pairs, B even)
+                g = [[i - c0 for i in grp] for grp in groups if c0 <= grp[0] < c0 + B]
+            pcm, n, fixed = self.engine.synthesize([cond_mel] * len(chunk), chunk, keys=keys * len(chunk),
+                                                   vocoder_groups=g, **dec)
+            pcm = pcm.cpu()
+            pcm_rows += [pcm[i, : int(n[i])] for i in range(pcm.shape[0])]
+            codes_all += fixed
+            raw = self.engine.last_raw_codes
+            self._hit_limit = self._hit_limit or bool((raw != self.stop_mel_token).all(axis=1).any())
+        return pcm_rows, codes_all
+
+    def _finish(self, pcm_rows, output_path, t0, cond_frames, label=""):
+        wav = torch.cat(pcm_rows) if pcm_rows else torch.zeros(0, dtype=torch.int16)
+        end = time.perf_counter()
+        wav_len = wav.shape[0] / SR
+        print(f">> Reference audio length: {cond_frames * 256 / SR:.2f} seconds")
+        print(f">> Total {label}inference time: {end - t0:.2f} seconds")
+        print(f">> Generated audio length: {wav_len:.2f} seconds")
+        if wav_len > 0:
+            print(f">> {'[fast] ' if label else ''}RTF: {(end - t0) / wav_len:.4f}")
+        data = wav.numpy().astype(np.int16).reshape(-1, 1)
+        if output_path:
+            if os.path.isfile(output_path):
+                os.remove(output_path)
+                print(">> remove old wav file:", output_path)
+            if os.path.dirname(output_path) != "":
+                os.makedirs(os.path.dirname(output_path), exist_ok=True)
+            save_wav_int16(output_path, data, SR)
+            print(">> wav file saved to:", output_path)
+            return output_path
+        return (SR, data)
+
+    def _warn_truncated(self, codes_raw_hit_limit, max_mel_tokens, max_text_tokens_per_sentence):
+        if codes_raw_hit_limit:
+            warnings.warn(f"WARN: generation stopped due to exceeding `max_mel_tokens` ({max_mel_tokens}). "
+                          f"Consider reducing `max_text_tokens_per_sentence`({max_text_tokens_per_sentence}) "
+                          "or increasing `max_mel_tokens`.", category=RuntimeWarning)
+
+    def _synthesize(self, audio_prompt, text, output_path, verbose, max_tokens, gen, fast, bucket_max_size=4):
+        print(">> start fast inference..." if fast else ">> start inference...")
+        self._set_gr_progress(0, "start fast inference..." if fast else "start inference...")
+        if verbose:
+            print(f"origin text:{text}")
+        t0 = time.perf_counter()
+        cond_mel = self._prompt(audio_prompt)
+        self._set_gr_progress(0.1, "text processing...")
+        tokens = self.tokenizer.tokenize(text)
+        sentences = self.tokenizer.split_sentences(tokens, max_tokens)
+        if verbose:
+            print("text token count:", len(tokens))
+            print("sentences count:", len(sentences))
+            print("max_text_tokens_per_sentence:", max_tokens)
+            print(*sentences, sep="\n")
+        dec = self._decoding(dict(gen))
+        order = list(range(len(sentences)))
+        if fast:  # bucketing only decides which sentences share a GPT batch in the reference; every
+            # sentence is batched here, so it only drops empty sentences (as the reference does)
+            order = [d["idx"] for b in self.bucket_sentences(sentences, bucket_max_size) for d in b]
+            order.sort()
+        ids = [torch.tensor(self.tokenizer.convert_tokens_to_ids(sentences[i]), dtype=torch.int32) for i in order]
+        if not ids:
+            return self._finish([], output_path, t0, cond_mel.shape[-1], "fast " if fast else "")
+        groups = None
+        if fast:  # BigVGAN decodes the latents of consecutive sentence pairs as one sequence
+            groups = [list(range(i, min(i + 2, len(ids)))) for i in range(0, len(ids), 2)]
+        self._set_gr_progress(0.2, "gpt inference speech...")
+        self._hit_limit = False
+        pcm_rows, codes = self._run(cond_mel, ids, dec, groups)
+        self._warn_truncated(self._hit_limit, dec["max_mel_tokens"], max_tokens)
+        self._set_gr_progress(0.9, "save audio...")
+        return self._finish(pcm_rows, output_path, t0, cond_mel.shape[-1], "fast " if fast else "")
+
+    # ------------------------------------------------------------------ public API
+    def infer_fast(self, audio_prompt, text, output_path, verbose=False, max_text_tokens_per_sentence=100,
+                   sentences_bucket_max_size=4, **generation_kwargs):
+        """infer.py:278-497 (sentence pairs vocoded together; one batched GPT pass for all sentences)."""
+        return self._synthesize(audio_prompt, text, output_path, verbose, max_text_tokens_per_sentence,
+                                generation_kwargs, fast=True, bucket_max_size=sentences_bucket_max_size)
+
+    def infer(self, audio_prompt, text, output_path, verbose=False, max_text_tokens_per_sentence=120,
+              **generation_kwargs):
+        """infer.py:500-660 -> output_path (16-bit PCM 24 kHz wav written) or (24000, int16 [T, 1])."""
+        return self._synthesize(audio_prompt, text, output_path, verbose, max_text_tokens_per_sentence,
+                                generation_kwargs, fast=False)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    from .cli import main
+    sys.exit(main())

@@ -37,6 +37,20 @@ def remove_long_silence(codes: np.ndarray, stop: int, silent_token: int = 52, ma
     return codes[:n]
 
 
+def concat_latents(latent: torch.Tensor, lens: torch.Tensor, spk: torch.Tensor, groups: List[List[int]]):
+    """latent [B, T, D] (rows valid up to lens[b]) -> [G, T', D] with group g = time-concatenation of
+    its members' valid rows (``torch.cat(items, dim=1)``, infer.py:454)."""
+    n = [int(v) for v in lens]
+    glen = [sum(n[i] for i in g) for g in groups]
+    out = latent.new_zeros(len(groups), max(glen), latent.shape[2])
+    for gi, g in enumerate(groups):
+        t = 0
+        for i in g:
+            out[gi, t: t + n[i]] = latent[i, : n[i]]
+            t += n[i]
+    return out, torch.tensor(glen, dtype=lens.dtype), spk[[g[0] for g in groups]]
+
+
 class BatchedTTS:
     def __init__(self, gpt_state_dict, bigvgan_state_dict, cfg, device="cuda", dtype: str = "bf16",
                  max_kv: Optional[int] = None):
@@ -52,7 +66,16 @@ class BatchedTTS:
     def prompt_features(self, mels: Sequence[torch.Tensor], keys: Optional[Sequence[object]] = None):
         """per-prompt conditioning (conds [32, D]) and speaker embedding ([spk_dim]); cached by key."""
         feats: Dict[int, tuple] = {}
-        todo = [i for i in range(len(mels)) if keys is None or keys[i] not in self._prompt_cache]
+        # one evaluation per distinct prompt: a prompt's features must not depend on how many
+        # utterances share it in this call (batched-conv rounding differs with the batch size)
+        first: Dict[object, int] = {}
+        todo = []
+        for i in range(len(mels)):
+            if keys is None:
+                todo.append(i)
+            elif keys[i] not in self._prompt_cache and keys[i] not in first:
+                first[keys[i]] = i
+                todo.append(i)
         by_len: Dict[int, List[int]] = {}  # equal-length prompts share one batched call
         for i in todo:
             by_len.setdefault(int(mels[i].shape[-1]), []).append(i)
@@ -70,10 +93,14 @@ class BatchedTTS:
     @torch.no_grad()
     def synthesize(self, mels: Sequence[torch.Tensor], texts: Sequence[torch.Tensor], max_mel_tokens: int = 600,
                    repetition_penalty: float = 10.0, min_new_tokens: int = 0, keys=None, use_graph: bool = True,
-                   timings: Optional[dict] = None):
+                   timings: Optional[dict] = None, vocoder_groups: Optional[List[List[int]]] = None, **sampling):
         """mels[b]: prompt log-mel [1, 100, T_b]; texts[b]: token ids [L_b].
         -> (pcm int16 [B, Tmax] on device, sample lengths [B] (cpu), codes list).
-        ``timings``: if a dict is given, per-phase wall seconds are accumulated into it (adds syncs)."""
+        ``timings``: if a dict is given, per-phase wall seconds are accumulated into it (adds syncs).
+        ``sampling``: do_sample / temperature / top_k / top_p / seed (HipGPT.generate).
+        ``vocoder_groups``: utterance index lists whose latents are concatenated along time before the
+        vocoder (``infer_fast`` decodes pairs of sentences as one latent, infer.py:440-458); the pcm /
+        lengths then have one row per group (speaker embedding of the group's first member)."""
         import time
 
         def mark(name, t=[None]):
@@ -94,14 +121,17 @@ class BatchedTTS:
         for b, t in enumerate(texts):
             ids[b, : t.numel()] = t.reshape(-1).long()
         codes = self.gpt.generate(conds, ids.to(self.device), max_mel_tokens, repetition_penalty=repetition_penalty,
-                                  min_new_tokens=min_new_tokens, use_graph=use_graph)
+                                  min_new_tokens=min_new_tokens, use_graph=use_graph, **sampling)
         mark("gpt_generate")
         rows = codes.cpu().numpy()
+        self.last_raw_codes = rows  # [B, n] as generated (finished rows padded with the stop token)
         fixed = [torch.from_numpy(remove_long_silence(rows[b], self.stop)) for b in range(B)]
         fixed = [f if f.numel() > 0 else torch.tensor([self.stop]) for f in fixed]  # degenerate: nothing generated
         mark("remove_long_silence")
         latent, lens = self.gpt.latent(conds, [t.reshape(-1) for t in texts], fixed)
         mark("latent_pass")
+        if vocoder_groups is not None:
+            latent, lens, spk = concat_latents(latent, lens, spk, vocoder_groups)
         _, pcm = self.vocoder.forward(latent, lens, spk)
         mark("vocoder")
         return pcm, (lens.long() * HOP), fixed
