@@ -8,9 +8,13 @@ teacher-forced latent pass, BigVGAN2 -> int16 PCM; with N>1 ranks the finished w
 to rank 0 over RCCL (utterances shard data-parallel, weak scaling).  Inputs are resident in HBM when
 the timed region starts; weights are seeded random-init IndexTTS-1.5 (no checkpoints are available).
 
-Also reports, for the dominant kernel (the MFMA implicit-GEMM that runs every BigVGAN conv), its
-achieved TFLOP/s from HIP events over the timed region, and a CPU baseline: the fp32 oracle (a CPU
-restatement of the reference path) on a bounded sample, on this host's cores.
+Also reports ``roofline``: the MFMA implicit-GEMM that runs every BigVGAN conv (the largest
+eagerly-launched kernel family), achieved TFLOP/s from HIP events around each launch over the timed
+region, its algorithmic bytes per launch and, when profiles/traffic_r01.json exists, the HBM bytes per
+launch from the rocprofv3 PMC passes (profiles/pmc_vocoder.py); ``roofline_gpt_decode``: the
+hipGraph-replayed GPT decode step (weights + KV cache bytes per step / step time, HIP events around
+each replay); and a CPU baseline: the fp32 oracle (a CPU restatement of the reference path) on a
+bounded sample, on this host's cores.
 """
 import argparse
 import json
@@ -38,10 +42,11 @@ class KernelTimer:
     def __init__(self):
         self.events = []
         self.flops = 0.0
+        self.bytes = 0.0
         self.launches = 0
         self.enabled = False
 
-    def wrap(self, fn, flops):
+    def wrap(self, fn, flops, nbytes=0.0):
         if not self.enabled:
             return fn()
         s = torch.cuda.current_stream()
@@ -51,6 +56,7 @@ class KernelTimer:
         b.record(s)
         self.events.append((a, b))
         self.flops += flops
+        self.bytes += nbytes
         self.launches += 1
         return r
 
@@ -65,15 +71,20 @@ def install_conv_timer(voc, timer):
 
     def timed(c, x, y, lens, **kw):
         rows = voc.rows  # host-side count of valid rows (no device sync)
-        return timer.wrap(lambda: orig(c, x, y, lens, **kw), 2.0 * rows * c.cout * c.cin * c.ntaps)
+        # algorithmic bytes: valid input rows read once, output rows written once, residual rows read,
+        # the packed weights read once (bf16)
+        nres = sum(kw.get(k) is not None for k in ("r1", "r2"))
+        nbytes = 2.0 * rows * (c.cin + c.cout * (1 + nres)) + 2.0 * c.ntaps * c.cin * c.cout
+        return timer.wrap(lambda: orig(c, x, y, lens, **kw), 2.0 * rows * c.cout * c.cin * c.ntaps, nbytes)
 
     voc._conv = timed
 
 
-def make_inputs(cfg, rank, B, L, frames):
+def make_inputs(cfg, indices, L, frames):
+    """synthetic utterances by global index (prompt mel + text ids seeded by the index)."""
     mels, texts = [], []
-    for i in range(B):
-        g = np.random.default_rng(2 + rank * B + i)
+    for i in indices:
+        g = np.random.default_rng(2 + i)
         mels.append(torch.from_numpy(g.normal(-4.0, 2.0, (1, 100, frames)).astype(np.float32)))
         texts.append(torch.from_numpy(g.integers(2, int(cfg.gpt.number_text_tokens), L).astype(np.int64)))
     return mels, texts
@@ -91,7 +102,7 @@ def cpu_baseline(cfg, gsd, vsd, B, N, L, frames):
     orc = GPTOracle(gt, cfg.gpt)
     voc = BigVGANOracle(vsd, cfg.bigvgan)
     vt = {k: v for k, v in fold_weight_norm(vsd).items()}
-    mels, texts = make_inputs(cfg, 0, B, L, frames)
+    mels, texts = make_inputs(cfg, range(B), L, frames)
     with torch.no_grad():
         t0 = time.perf_counter()
         mel = torch.cat(mels, 0)
@@ -120,8 +131,8 @@ def main():
     ap.add_argument("--text-len", type=int, default=48)
     ap.add_argument("--prompt-frames", type=int, default=511)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-codes", type=int, default=32)
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-codes", type=int, default=96)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
     args = ap.parse_args()
@@ -135,6 +146,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from indextts.pipeline import BatchedTTS, SR
+    from indextts.sharding import gather_waveforms, shard
     from indextts.utils.config import default_config_path, load_config
     from indextts.utils.synthetic import bigvgan_state_dict, gpt_state_dict
 
@@ -145,22 +157,15 @@ def main():
     tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + L + 2 + 1 + N + 8)
     timer = KernelTimer()
     install_conv_timer(tts.vocoder, timer)
-    mels, texts = make_inputs(cfg, rank, B, L, args.prompt_frames)
+    # global batch of B * world utterances; utterance i runs on rank i % world (weak scaling)
+    mels, texts = make_inputs(cfg, shard(B * world, world, rank), L, args.prompt_frames)
     mels = [m.to(dev) for m in mels]
     texts = [t.to(dev) for t in texts]
 
     def step():
         pcm, lens, _ = tts.synthesize(mels, texts, max_mel_tokens=N, min_new_tokens=N)
-        if world > 1:
-            raw = pcm.contiguous().view(torch.uint8).reshape(-1)
-            n = torch.tensor([raw.numel()], device=dev, dtype=torch.int64)
-            sizes = [torch.zeros_like(n) for _ in range(world)]
-            dist.all_gather(sizes, n)
-            cap = int(max(int(s) for s in sizes))
-            buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
-            buf[: raw.numel()] = raw
-            gl = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-            dist.gather(buf, gl, dst=0)
+        if world > 1:  # the one collective: finished int16 waveforms to rank 0, in utterance order
+            gather_waveforms([pcm[b, : int(lens[b])] for b in range(B)], B * world, dev)
         return float(lens.sum()) / SR
 
     for _ in range(args.warmup):
@@ -169,6 +174,8 @@ def main():
     if world > 1:
         dist.barrier()
     timer.enabled = not args.no_kernel_timing
+    if timer.enabled:
+        tts.gpt.step_events = []  # HIP events around every decode-step graph replay
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     audio = 0.0
@@ -180,6 +187,17 @@ def main():
     dt = time.perf_counter() - t0
     timer.enabled = False
     k_ms, k_flops, k_n = timer.result()
+    step_ev, tts.gpt.step_events = tts.gpt.step_events, None
+    dec = None
+    if step_ev:
+        d_ms = sum(a.elapsed_time(b) for a, b, _, _ in step_ev)
+        d_bytes = sum(tts.gpt.step_weight_bytes + keys * tts.gpt.kv_bytes_per_key for _, _, _, keys in step_ev)
+        gbs = d_bytes / (d_ms * 1e-3) / 1e9
+        dec = {"kernel": "GPT decode step (hipGraph: 20 x [c_attn GEMM, attention, c_proj GEMM, reduce+LN, "
+                         "c_fc GEMM, mlp.c_proj GEMM, reduce+LN] + mel_head GEMM + sampler)", "bound": "hbm",
+               "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+               "traffic": None, "launches": len(step_ev), "avg_launch_us": round(1e3 * d_ms / len(step_ev), 2),
+               "algorithmic_bytes_per_launch": round(d_bytes / len(step_ev)), "share_of_step": round(d_ms / (1e3 * dt), 3)}
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -195,6 +213,7 @@ def main():
             "achieved": None if achieved is None else round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / PEAK_BF16_TFLOPS, 4),
             "traffic": None, "launches": k_n, "avg_launch_us": round(1e3 * k_ms / max(k_n, 1), 2),
+            "algorithmic_bytes_per_launch": round(timer.bytes / max(k_n, 1)),
             "share_of_step": round(k_ms / (1e3 * dt), 3)}
     tf = os.path.join(REPO, "profiles", "traffic_r01.json")
     if os.path.exists(tf):
@@ -217,6 +236,7 @@ def main():
                                "latent pass, BigVGAN2 -> int16", "global_batch": B * world, "seq_len": N,
                    "parallelism": f"dp{world}"},
         "roofline": roof,
+        "roofline_gpt_decode": dec,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -117,7 +117,8 @@ int itts_sample_embed(const float* logits, int64_t ldl, int V, uint8_t* seen, ui
 /* do_sample=True variant: Temperature -> TopK (1..64, ties at the k-th value kept) -> TopP warpers
  * and a multinomial draw (HF 4.36 `sample`; infer.py:535-543 defaults top_k 30 / top_p 0.8).
  * top_k == 0 (with top_p == 1): draw from the full softmax.  RNG: counter hash of
- * (seed = tstate[2] | tstate[3] << 32, row, column) -- statistical parity with torch.multinomial. */
+ * (seed = tstate[2] | tstate[3] << 32, row + tstate[1], column) -- statistical parity with
+ * torch.multinomial; tstate[1] = global index of this launch's row 0 (row chunks on several streams). */
 int itts_sample_topk_embed(const float* logits, int64_t ldl, int V, uint8_t* seen, uint8_t* done, int32_t* codes,
                            int64_t ldc, const int32_t* tstate, int col_delta, int min_new, int stop, float penalty,
                            float temperature, int top_k, float top_p, const float* emb, const float* pos_emb,

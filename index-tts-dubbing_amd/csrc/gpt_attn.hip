@@ -4,9 +4,10 @@
 //
 // 1. itts_attn_decode: one new token per sequence.  Appends its k/v (from the QKV projection, f32)
 //    into the KV cache at index kv_base + *t (device counter -> hipGraph-replayable), then attends
-//    over keys [pad_b, kv_base + *t].  One 256-thread workgroup per (head, sequence); scores use
-//    8 lanes per key (one 1 KiB coalesced wave load = 8 key rows), softmax via workgroup reductions,
-//    P.V with 8 lanes per key-row slice reduced through LDS.
+//    over keys [pad_b, kv_base + *t].  One 256-thread workgroup per (head, sequence), ONE pass over
+//    the cache: 8 lanes per key row (one 1 KiB coalesced wave load = 8 rows of K, one of V), online
+//    softmax per 8-lane group, log-sum-exp merge of the 32 groups through LDS.  HBM-bound: it
+//    streams 2 * S * 64 * sizeof(cache) bytes per (sequence, head).
 // 2. itts_attn_prefill: variable-length causal attention over packed sequences (prefill of the
 //    prompt block, and the teacher-forced latent pass).  One thread per query, K/V staged through
 //    LDS in 32-key blocks, block-wise online softmax; optionally writes K/V into the decode cache.
@@ -33,18 +34,7 @@ __device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]
   }
 }
 
-__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
-  v = is_max ? wave_max(v) : wave_sum(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  float r = red[0];
-  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
-  return r;
-}
-
-constexpr int kMaxKeys = 2048;
+constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is the caller's
 
 template <typename TC, typename TO>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv,
@@ -53,8 +43,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
                                                           int kv_base, const int32_t* __restrict__ tstate,
                                                           TO* __restrict__ out, int64_t ldo, int H) {
   __shared__ float qs[kHD], kn[kHD], vn[kHD];
-  __shared__ float sc[kMaxKeys];
-  __shared__ float red[8];
+  __shared__ float gm[32], gl[32];
   __shared__ float pv[32][kHD + 1];
   const int h = blockIdx.x, b = blockIdx.y;
   const int D = H * kHD;
@@ -66,7 +55,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
   TC* Vc = cache_v + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
   if (threadIdx.x < kHD) {
     const int d = threadIdx.x;
-    qs[d] = row[d];
+    qs[d] = row[d] * 0.125f;  // 1/sqrt(64), exact
     const float k = row[D + d], v = row[2 * D + d];
     kn[d] = k;
     vn[d] = v;
@@ -74,75 +63,79 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
     St<TC>::st(Vc + (int64_t)kidx * kHD + d, v);
   }
   __syncthreads();
+  // 32 groups of 8 lanes; group g owns keys g, g+32, ...; lane d8 holds dims 8*d8 .. 8*d8+7.
+  // Single pass: K and V rows of KB keys are loaded together, scores via 8-lane shuffles, and an
+  // online softmax per group (running max m, sum l, partial output o); groups merge through LDS.
   const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
   float q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) q[e] = qs[8 * d8 + e];
-  // scores for keys p0 .. kidx (the new key from LDS so the just-written cache line is never re-read)
-  // KB key rows per 8-lane group per round, all loads issued before use (latency hiding)
   constexpr int KB = 8;
-  float lmax = -INFINITY;
+  float m = -INFINITY, l = 0.f;
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nk; j0 += 32 * KB) {
-    float k[KB][8];
+    float k[KB][8], v[KB][8];
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
       const int j = j0 + 32 * u + g;
-      if (j < nk && p0 + j != kidx) load8<TC>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8, k[u]);
-      else
+      if (j < nk && p0 + j != kidx) {
+        load8<TC>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8, k[u]);
+        load8<TC>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8, v[u]);
+      } else {  // the new key/value comes from LDS (never re-read the line just written)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) k[u][e] = kn[8 * d8 + e];
+        for (int e = 0; e < 8; ++e) {
+          k[u][e] = kn[8 * d8 + e];
+          v[u][e] = vn[8 * d8 + e];
+        }
+      }
     }
+    float s[KB];
+    float bm = -INFINITY;
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
-      const int j = j0 + 32 * u + g;
       float part = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) part = fmaf(q[e], k[u][e], part);
       part += __shfl_xor(part, 1, 64);
       part += __shfl_xor(part, 2, 64);
       part += __shfl_xor(part, 4, 64);
-      if (j < nk && d8 == 0) {
-        const float s = part * 0.125f;
-        sc[j] = s;
-        lmax = fmaxf(lmax, s);
-      }
+      s[u] = (j0 + 32 * u + g < nk) ? part : -INFINITY;
+      bm = fmaxf(bm, s[u]);
     }
-  }
-  const float mx = block_reduce(lmax, red, true);
-  float lsum = 0.f;
-  for (int j = threadIdx.x; j < nk; j += 256) {
-    const float e = __expf(sc[j] - mx);
-    sc[j] = e;
-    lsum += e;
-  }
-  const float inv = 1.0f / block_reduce(lsum, red, false);  // includes a barrier: sc[] complete
-  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 0; j0 < nk; j0 += 32 * KB) {
-    float v[KB][8];
+    if (bm == -INFINITY) continue;  // this group has no valid key in the round
+    const float mn = fmaxf(m, bm);
+    const float corr = __expf(m - mn);  // m = -inf -> 0
+    l *= corr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= corr;
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
-      const int j = j0 + 32 * u + g;
-      if (j < nk && p0 + j != kidx) load8<TC>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8, v[u]);
-      else
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[u][e] = vn[8 * d8 + e];
-    }
-#pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      const int j = j0 + 32 * u + g;
-      const float p = j < nk ? sc[j] : 0.f;
+      const float p = __expf(s[u] - mn);
+      l += p;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = fmaf(p, v[u][e], o[e]);
     }
+    m = mn;
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) pv[g][8 * d8 + e] = o[e];
+  if (d8 == 0) {
+    gm[g] = m;
+    gl[g] = l;
+  }
   __syncthreads();
   if (threadIdx.x < kHD) {
-    float s = 0.f;
+    float M = -INFINITY;
 #pragma unroll 8
-    for (int i = 0; i < 32; ++i) s += pv[i][threadIdx.x];
-    St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, s * inv);
+    for (int i = 0; i < 32; ++i) M = fmaxf(M, gm[i]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) {
+      const float w = __expf(gm[i] - M);  // empty group: exp(-inf) = 0
+      L = fmaf(gl[i], w, L);
+      acc = fmaf(pv[i][threadIdx.x], w, acc);
+    }
+    St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, acc / L);
   }
 }
 
@@ -233,7 +226,7 @@ extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, void* cache_k, 
   ITTS_REQUIRE(B >= 0 && H > 0, fn, "bad sizes");
   if (B == 0) return 0;
   ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && out, fn, "null pointer");
-  ITTS_REQUIRE(smax <= kMaxKeys && cache_hs >= (int64_t)smax * kHD, fn, "cache capacity exceeds 2048 keys");
+  ITTS_REQUIRE(smax <= kMaxKeys && cache_hs >= (int64_t)smax * kHD, fn, "bad cache capacity");
   dim3 grid(H, B);
   hipStream_t s = itts::as_stream(stream);
 #define ITTS_AD(TC, TO)                                                                                          \

@@ -6,7 +6,7 @@
 //   * sampling (do_sample=True, num_beams=1; HF 4.36 `sample`): Temperature -> TopK -> TopP warpers
 //     (HF:generation/logits_process.py TemperatureLogitsWarper / TopKLogitsWarper / TopPLogitsWarper),
 //     softmax, one multinomial draw per row.  The draw uses a counter-based hash RNG keyed by
-//     (seed, row, column) with the seed in device memory (tstate[2..3]) so a captured hipGraph
+//     (seed, global row = tstate[1] + row, column) with the seed in device memory (tstate[2..3]) so a captured hipGraph
 //     replays it; the distribution equals torch's, the individual draws do not (torch's CPU/GPU
 //     Philox streams differ anyway), so sampling parity is statistical (tests/test_gpu_gpt.py).
 //   * finished rows emit the pad token (= stop 8193)
@@ -186,7 +186,8 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
   const int b = blockIdx.x;
   const int col = p.tstate[0] + p.col_delta;
   const uint64_t seed = (uint64_t)(uint32_t)p.tstate[2] | ((uint64_t)(uint32_t)p.tstate[3] << 32);
-  const uint64_t key = mix64(seed ^ mix64(((uint64_t)b << 32) | (uint32_t)col));
+  const uint64_t row = (uint64_t)(uint32_t)(b + p.tstate[1]);  // tstate[1]: global index of row 0
+  const uint64_t key = mix64(seed ^ mix64((row << 32) | (uint32_t)col));
   const float* lr = p.logits + (int64_t)b * p.ldl;
   uint8_t* sr = p.seen + (int64_t)b * p.V;
   float best = -INFINITY;

@@ -82,8 +82,13 @@ class HipGPT:
             self.layers.append(ly)
         self.head_w = self._pack(sd["mel_head.weight"].float().contiguous(), igemm=False)
         self.head_b = f32("mel_head.bias")
-        self._state = None
-        self._graph = None
+        self._lanes = {}  # lane index -> decode state, captured graph, stream
+        self.step_events = None  # set to a list to time every decode step with HIP events (bench.py)
+        # algorithmic HBM bytes of one decode step: every weight byte once (+ per-key KV bytes)
+        eb = 2 if dtype == "bf16" else 4
+        self.step_weight_bytes = sum(eb * ly.w[n]["N"] * ly.w[n]["K"] for ly in self.layers for n in ly.w) \
+            + eb * self.head_w["N"] * self.head_w["K"]
+        self.kv_bytes_per_key = self.L * self.H * 64 * 2 * eb  # the K and V rows of one key, all layers
 
     # ---------------- weights ----------------
     def _pack(self, wt: torch.Tensor, igemm: bool = True):
@@ -301,54 +306,125 @@ class HipGPT:
             None if ln2 is None else ln2[1].data_ptr(), _hip.dtype_code(h), _hip.stream_ptr()),
             "itts_residual_reduce_ln")
 
-    # ---------------- public: greedy generate ----------------
+    # ---------------- public: generate ----------------
+    # Row chunks ("lanes") decode concurrently, each on its own HIP stream with its own captured
+    # graph and state: one decode step is a chain of ~150 small dependent kernels (latency-bound at
+    # batch 32), so two independent chains keep more of the GPU busy; the second lane re-reads each
+    # layer's weights shortly after the first, out of the 256 MiB Infinity Cache.  Rows never
+    # interact, so the ids do not depend on the lane split.
+    LANES = 1  # measured: 2 lanes of 16 rows are slower than 1 lane of 32 (half-size steps cost nearly as much)
+    MIN_LANE_ROWS = 8
+
+    def _lane_bounds(self, B: int, lanes: Optional[int]):
+        n = self.LANES if lanes is None else max(1, int(lanes))
+        n = max(1, min(n, B // self.MIN_LANE_ROWS)) if lanes is None else min(n, B)
+        step = (B + n - 1) // n
+        return [(r, min(B, r + step)) for r in range(0, B, step)]
+
+    def _lane(self, i: int, rows: int, max_new: int, s: int):
+        lanes = self.__dict__.setdefault("_lanes", {})
+        ln = lanes.get(i)
+        key = (rows, max_new, s)
+        if ln is None or ln["key"] != key:
+            if ln is not None:  # free the old lane before allocating (KV caches can be large)
+                lanes.pop(i)
+                del ln
+                torch.cuda.empty_cache()
+            ln = {"key": key, "st": self._alloc_state(rows, max_new), "graph": None,
+                  "stream": lanes.get(("stream", i)) or torch.cuda.Stream(self.dev)}
+            lanes[("stream", i)] = ln["stream"]
+            lanes[i] = ln
+        return ln
+
     @torch.no_grad()
     def generate(self, conds: torch.Tensor, text_ids: torch.Tensor, max_new_tokens: int,
                  repetition_penalty: float = 10.0, min_new_tokens: int = 0, use_graph: bool = True,
                  check_every: int = 16, forced_codes: Optional[torch.Tensor] = None, do_sample: bool = False,
                  temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
-                 seed: Optional[int] = None) -> torch.Tensor:
+                 seed: Optional[int] = None, lanes: Optional[int] = None) -> torch.Tensor:
         """Greedy (do_sample=False) or top-k/top-p sampling (do_sample=True; num_beams=1) decode
         -> codes [B, n] int64 on the device, finished rows padded with the stop token, n = steps until
         every row stopped (or max_new_tokens).  ``seed`` (default: drawn from torch's CPU generator)
-        keys the device RNG, so a fixed seed reproduces the draws."""
+        keys the device RNG (by global row), so a fixed seed reproduces the draws for any lane split."""
         emb, pad, s = self.prepare_inputs(conds, text_ids)
         B = emb.shape[0]
         assert s + 1 + max_new_tokens <= self.max_kv, "KV capacity exceeded"
-        key = (B, max_new_tokens, s)
-        if self._state is None or self._state["key"] != key:
-            self._state = self._alloc_state(B, max_new_tokens)
-            self._state["key"] = key
-            self._graph = None
-        st = self._state
+        sampling = (float(temperature), int(top_k), float(top_p)) if do_sample else None
+        if do_sample and seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None)
+        main = torch.cuda.current_stream(self.dev)
+        work = []
+        for i, (r0, r1) in enumerate(self._lane_bounds(B, lanes)):
+            ln = self._lane(i, r1 - r0, max_new_tokens, s)
+            ln["stream"].wait_stream(main)  # inputs prepared on the caller's stream
+            with torch.cuda.stream(ln["stream"]):
+                self._start_lane(ln, emb[r0:r1], pad[r0:r1], s, r0, sampling, seed,
+                                 None if forced_codes is None else forced_codes[r0:r1], min_new_tokens,
+                                 repetition_penalty, use_graph and max_new_tokens > 1, gkey)
+            work.append(ln)
+        steps = 1
+        ev = self.step_events  # optional instrumentation: HIP events around each lane's step
+        keys0 = [int((r1 - r0) * (s + 2)) - int(pad[r0:r1].sum()) for r0, r1 in self._lane_bounds(B, lanes)] \
+            if ev is not None else None
+        while steps < max_new_tokens:
+            for li, ln in enumerate(work):
+                with torch.cuda.stream(ln["stream"]):
+                    if ev is not None:
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                    if ln["graph_ok"]:
+                        ln["graph"][0].replay()
+                    else:
+                        self._decode_step(ln["st"], min_new_tokens, repetition_penalty)
+                    if ev is not None:
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e1.record()
+                        # keys attended this step, summed over the lane's rows: s + 2 + r - pad_b
+                        ev.append((e0, e1, ln["st"]["B"], keys0[li] + ln["st"]["B"] * (steps - 1)))
+            steps += 1
+            if steps % check_every == 0:
+                done = True
+                for ln in work:
+                    with torch.cuda.stream(ln["stream"]):
+                        done = done and bool(ln["st"]["done"].all())
+                if done:
+                    break
+        for ln in work:
+            main.wait_stream(ln["stream"])
+        codes = torch.cat([ln["st"]["codes"][:, :steps] for ln in work], 0).long()
+        hit = codes == self.stop_mel
+        if bool(hit.any(dim=1).all()):
+            n = int(hit.int().argmax(dim=1).max()) + 1
+            codes = codes[:, :n]
+        return codes
+
+    def _start_lane(self, ln, emb, pad, s, row0, sampling, seed, forced, min_new, penalty, use_graph, gkey):
+        """reset one lane's decode state, run its prefill + first token, (re)capture its graph."""
+        st = ln["st"]
+        B = st["B"]
         st["s"] = s
         st["pad"].copy_(pad)  # never rebind: the captured graph holds this pointer
         st["seen"].zero_()
         st["seen"][:, 1] = 1
         st["seen"][:, self.start_mel] = 1
         st["done"].zero_()
-        st["t"].zero_()
         st["codes"].fill_(self.stop_mel)
-        st["sampling"] = (float(temperature), int(top_k), float(top_p)) if do_sample else None
-        if do_sample:
-            if seed is None:
-                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-            seed &= (1 << 64) - 1
-            lo, hi = seed & 0xFFFFFFFF, seed >> 32
-            st["t"][2:4].copy_(torch.tensor([lo - (1 << 32) if lo >= 1 << 31 else lo,
-                                             hi - (1 << 32) if hi >= 1 << 31 else hi], dtype=torch.int32))
-        gkey = (min_new_tokens, repetition_penalty, st["sampling"])
-        if forced_codes is not None:  # teacher forcing (tests): feed these ids, record the argmax ids
-            fc = torch.full((B, max_new_tokens), self.stop_mel, dtype=torch.int32, device=self.dev)
-            fc[:, : forced_codes.shape[1]] = forced_codes.to(self.dev, torch.int32)
-            if st.get("forced") is None or st["forced"].shape != fc.shape:
+        st["sampling"] = sampling
+        sd = [0, 0] if seed is None else [(seed >> 32 * i) & 0xFFFFFFFF for i in range(2)]
+        sd = [v - (1 << 32) if v >= 1 << 31 else v for v in sd]
+        st["t"].copy_(torch.tensor([0, row0, sd[0], sd[1]], dtype=torch.int32))
+        if forced is not None:  # teacher forcing (tests): feed these ids, record the chosen ids
+            fc = torch.full((B, st["max_new"]), self.stop_mel, dtype=torch.int32, device=self.dev)
+            fc[:, : forced.shape[1]] = forced.to(self.dev, torch.int32)
+            if st.get("forced") is None:
                 st["forced"] = fc
-                self._graph = None
+                ln["graph"] = None
             else:
                 st["forced"].copy_(fc)
         elif st.get("forced") is not None:
             st["forced"] = None
-            self._graph = None
+            ln["graph"] = None
         # ---- prefill over [B, s+1] rows ----
         M = B * (s + 1)
         x = emb.reshape(M, self.D).contiguous()
@@ -361,47 +437,28 @@ class HipGPT:
             self._gemm(st["h"][:B], self.head_w, st["logits"], bias=self.head_b)
         else:
             self._dg(st["h"], self.head_w, B, self.head_b, st["logits"])
-        self._sample(st, 0, min_new_tokens, repetition_penalty)
-        # ---- decode loop ----
-        steps = 1
-        graph_ok = use_graph and self._graph is not None and self._graph[1] == gkey
-        if use_graph and not graph_ok and max_new_tokens > 1:
-            self._capture(st, min_new_tokens, repetition_penalty)
-            self._graph = (self._graph[0], gkey)
-            graph_ok = True
-        while steps < max_new_tokens:
-            if graph_ok:
-                self._graph[0].replay()
-            else:
-                self._decode_step(st, min_new_tokens, repetition_penalty)
-            steps += 1
-            if steps % check_every == 0 and bool(st["done"].all()):
-                break
-        codes = st["codes"][:, :steps].long()
-        hit = codes == self.stop_mel
-        if bool(hit.any(dim=1).all()):
-            n = int(hit.int().argmax(dim=1).max()) + 1
-            codes = codes[:, :n]
-        return codes
+        self._sample(st, 0, min_new, penalty)
+        ln["graph_ok"] = False
+        if use_graph:
+            if ln["graph"] is None or ln["graph"][1] != gkey:
+                ln["graph"] = (self._capture(st, min_new, penalty), gkey)
+            ln["graph_ok"] = True
 
     def _capture(self, st, min_new, penalty):
         """Capture one decode step into a hipGraph; counters are device-side so replays advance."""
-        t_save = st["t"].clone()
-        x_save, h_save = st["x"].clone(), st["h"].clone()
-        seen_save, done_save, codes_save = st["seen"].clone(), st["done"].clone(), st["codes"].clone()
+        saved = {k: st[k].clone() for k in ("t", "x", "h", "seen", "done", "codes")}
+        cur = torch.cuda.current_stream(self.dev)
         s = torch.cuda.Stream(self.dev)
-        s.wait_stream(torch.cuda.current_stream(self.dev))
+        s.wait_stream(cur)
         with torch.cuda.stream(s):
             self._decode_step(st, min_new, penalty)  # warm-up (also validates launches)
-        torch.cuda.current_stream(self.dev).wait_stream(s)
-        # restore state mutated by the warm-up step
-        st["t"].copy_(t_save); st["x"].copy_(x_save); st["h"].copy_(h_save)
-        st["seen"].copy_(seen_save); st["done"].copy_(done_save); st["codes"].copy_(codes_save)
+        cur.wait_stream(s)
+        for k, v in saved.items():  # restore the state mutated by the warm-up step
+            st[k].copy_(v)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._decode_step(st, min_new, penalty)
-        self._graph = (g, (min_new, penalty))
-        # capture does not execute the kernels; state is intact
+        return g  # capture does not execute the kernels; state is intact
 
     # ---------------- latent pass ----------------
     @torch.no_grad()

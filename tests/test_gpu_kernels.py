@@ -96,3 +96,47 @@ def test_residual_reduce_ln_matches_torch():
     hr = F.layer_norm(F.layer_norm(xr, (D,), g1, b1, 1e-5), (D,), g2, b2, 1e-5)
     torch.testing.assert_close(xd.cpu(), xr, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(h.float().cpu(), hr, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("S,cache", [(1, "bf16"), (37, "bf16"), (300, "bf16"), (1000, "bf16"), (300, "f32")])
+def test_attn_decode_matches_torch(S, cache):
+    """One decode step: appends k/v at kv_base + t, then softmax(q k^T / 8 + pad mask) v over the
+    cached prefix; vs torch fp32 on the same (cache-rounded) keys/values.  |err| <= 2e-3 (bf16
+    output rounding) / 1e-5 (f32)."""
+    _hip, lib = _lib()
+    torch.manual_seed(S)
+    B, H, smax = 5, 16, S + 8
+    D = 64 * H
+    cdt = torch.bfloat16 if cache == "bf16" else torch.float32
+    kc = (torch.randn(B, H, smax, 64) * 0.5).to(cdt)
+    vc = torch.randn(B, H, smax, 64).to(cdt)
+    qkv = torch.randn(B, 3 * D)
+    pad = torch.tensor([0, 3, 0, min(7, S - 1), 1], dtype=torch.int32).clamp(max=S - 1)
+    kv_base, t = S - 1 - 2, 2  # new key lands at index S - 1
+    kd, vd = kc.clone().cuda(), vc.clone().cuda()
+    out = torch.zeros(B, D, dtype=cdt).cuda()
+    tst = torch.tensor([t, 0, 0, 0], dtype=torch.int32).cuda()
+    qkv_d, pad_d = qkv.cuda(), pad.cuda()  # keep device temporaries alive until the kernel ran
+    _hip.check(lib.itts_attn_decode(qkv_d.data_ptr(), 3 * D, kd.data_ptr(), vd.data_ptr(), kd.stride(0),
+                                    kd.stride(1), smax, pad_d.data_ptr(), kv_base, tst.data_ptr(),
+                                    out.data_ptr(), D, B, H, _hip.dtype_code(kd), _hip.dtype_code(out),
+                                    _hip.stream_ptr()), "attn_decode")
+    torch.cuda.synchronize()
+    kidx = S - 1
+    q = qkv[:, :D].view(B, H, 64)
+    kn, vn = qkv[:, D:2 * D].view(B, H, 64), qkv[:, 2 * D:].view(B, H, 64)
+    kr, vr = kc.float().clone(), vc.float().clone()
+    kr[:, :, kidx], vr[:, :, kidx] = kn, vn  # the kernel uses the exact f32 new k/v for the new key
+    ref = torch.zeros(B, H, 64)
+    for b in range(B):
+        p0 = int(pad[b])
+        sc = torch.einsum("hd,hsd->hs", q[b], kr[b, :, p0:kidx + 1]) / 8.0
+        ref[b] = torch.einsum("hs,hsd->hd", sc.softmax(-1), vr[b, :, p0:kidx + 1])
+    got = out.float().cpu().view(B, H, 64)
+    tol = 2e-2 if cache == "bf16" else 1e-5
+    assert float((got - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
+    # the cache row kidx now holds the new k/v (rounded to the cache dtype); nothing else changed
+    assert torch.equal(kd[:, :, kidx].cpu(), kn.to(cdt)) and torch.equal(vd[:, :, kidx].cpu(), vn.to(cdt))
+    keep = torch.ones(smax, dtype=torch.bool)
+    keep[kidx] = False
+    assert torch.equal(kd[:, :, keep].cpu(), kc[:, :, keep]) and torch.equal(vd[:, :, keep].cpu(), vc[:, :, keep])
