@@ -65,6 +65,16 @@ int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packe
                    const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy,
                    const int32_t* lengths, int B, int Tmax, int Cin, int Cout, int ntaps, const int32_t* tap_off,
                    int y_row_mul, int y_row_off, float alpha, int gelu, int out_dtype, void* stream);
+/* One AMPBlock1 conv of the narrow stages (C in {24, 48, 96} after padding to 32/64/96) with the
+ * preceding Activation1d fused in (log_alpha == NULL: no activation):
+ *   y[b][t][:] = alpha * (sum_j W_j . act(x)[b][t + tap_off[j]][:] + bias + r1[b][t][:] + r2[b][t][:])
+ * (models.py:65-74 `xt = c1(a1(x)); xt = c2(a2(xt)); x = xt + x`, :237-243 block mean).  bf16
+ * channel-last, 16-B aligned, channels / strides multiples of 8; weights in the igemm packing. */
+int itts_amp_conv_fwd(const void* x, int64_t x_sb, int64_t ldx, const float* up12, const float* down12,
+                      const float* log_alpha, const float* log_beta, const void* w_packed, const float* bias,
+                      const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy, const int32_t* lengths,
+                      int B, int Tmax, int Cin, int Cout, int ntaps, const int32_t* tap_off, float alpha,
+                      void* stream);
 /* conv_post (Conv1d(C->1, K, pad K/2), bias) + tanh (models.py:246-248), optionally also the int16
  * PCM of infer.py:627,653 (clamp(32767*wav, +-32767) truncated toward zero, quirk Q8). */
 int itts_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* w, float bias, int C, int K,

@@ -114,6 +114,8 @@ class _Act:
 
 
 class HipBigVGAN:
+    FUSED_CHANNELS = (24, 48)  # AMP stages run by itts_amp_conv_fwd (act fused; at C=96 separate kernels measured equal)
+
     def __init__(self, state_dict, cfg_bv, device="cuda"):
         self.lib = _hip.load()
         self.h = h = cfg_bv
@@ -154,6 +156,7 @@ class HipBigVGAN:
         self.post_k = wp.shape[-1]
         self.hop = int(np.prod([int(u) for u in h.upsample_rates]))
         self._bufs = {}
+        self.fused_amp = True  # narrow stages: activation fused into the conv (False: separate kernels)
 
     # ---------------- per-prompt (cached by the caller) ----------------
     @torch.no_grad()
@@ -185,6 +188,17 @@ class HipBigVGAN:
             x.data_ptr(), y.data_ptr(), a.up.data_ptr(), a.down.data_ptr(), a.alpha.data_ptr(), a.beta.data_ptr(),
             lens.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1, _hip.dtype_code(x), _hip.dtype_code(y),
             _hip.stream_ptr()), "itts_aa_snakebeta_fwd")
+
+    def _amp(self, c: _Conv, x, y, lens, a: _Act = None, r1=None, r2=None, alpha=1.0):
+        """y = alpha * (conv(act(x)) + bias + r1 + r2) in one launch (itts_amp_conv_fwd)."""
+        B, T, Cin = x.shape
+        Ty = y.shape[1]
+        _hip.check(self.lib.itts_amp_conv_fwd(
+            x.data_ptr(), T * Cin, Cin, None if a is None else a.up.data_ptr(),
+            None if a is None else a.down.data_ptr(), None if a is None else a.alpha.data_ptr(),
+            None if a is None else a.beta.data_ptr(), c.w.data_ptr(), c.bias.data_ptr(), _hip.ptr(r1), _hip.ptr(r2),
+            y.data_ptr(), Ty * y.shape[2], y.shape[2], lens.data_ptr(), B, T, Cin, c.cout, c.ntaps, c.offs,
+            float(alpha), _hip.stream_ptr()), "itts_amp_conv_fwd")
 
     def _conv(self, c: _Conv, x, y, lens, r1=None, r2=None, alpha=1.0, bias_b=None, ymul=1, yoff=0, Tq=None):
         B, T, Cin = x.shape
@@ -226,17 +240,21 @@ class HipBigVGAN:
             xs = self._buf("xs_b" if i % 2 == 0 else "xs_a", (B, Tn, C))
             for j, layers in enumerate(self.blocks[i]):
                 src = x_st
+                fused = self.fused_amp and C in self.FUSED_CHANNELS
                 for n, (a1, c1, a2, c2) in enumerate(layers):
-                    self._act(a1, src, t1, lens_n)
-                    self._conv(c1, t1, t2, lens_n)
-                    self._act(a2, t2, t1, lens_n)
-                    if n < len(layers) - 1:
-                        self._conv(c2, t1, cur, lens_n, r1=src)
-                        src = cur
+                    last_layer = n == len(layers) - 1
+                    alpha = (1.0 / self.nk) if (last_layer and j == self.nk - 1) else 1.0
+                    dst = xs if last_layer else cur
+                    r2 = xs if (last_layer and j > 0) else None
+                    if fused:  # activation fused into each conv's input staging (amp_conv.hip)
+                        self._amp(c1, src, t2, lens_n, a1)
+                        self._amp(c2, t2, dst, lens_n, a2, r1=src, r2=r2, alpha=alpha)
                     else:
-                        last = j == self.nk - 1
-                        self._conv(c2, t1, xs, lens_n, r1=src, r2=xs if j > 0 else None,
-                                   alpha=(1.0 / self.nk) if last else 1.0)
+                        self._act(a1, src, t1, lens_n)
+                        self._conv(c1, t1, t2, lens_n)
+                        self._act(a2, t2, t1, lens_n)
+                        self._conv(c2, t1, dst, lens_n, r1=src, r2=r2, alpha=alpha)
+                    src = dst
             cur_in, Tcur, lens = xs, Tn, lens_n
         t1 = self._buf("t1", cur_in.shape)
         self._act(self.act_post, cur_in, t1, lens)

@@ -134,3 +134,50 @@ def test_vocoder_ragged_batch_equals_single():
         ref = orc.forward(lat[b:b + 1, :L], spk[b:b + 1])[0, 0]
         rel = float(((w1[0].cpu() - ref) ** 2).mean().sqrt() / (ref ** 2).mean().sqrt())
         assert rel <= 2e-2, rel
+
+
+@pytest.mark.parametrize("C,k,d,use_act,nres,alpha", [(24, 7, 3, True, 1, 1.0), (48, 11, 5, True, 2, 1.0 / 3),
+                                                     (96, 3, 1, False, 0, 1.0), (24, 3, 1, True, 0, 1.0),
+                                                     (96, 11, 5, True, 1, 1.0), (48, 7, 1, False, 2, 0.5)])
+def test_amp_conv_matches_torch(C, k, d, use_act, nres, alpha):
+    """itts_amp_conv_fwd = alpha * (conv(act(x)) + bias + r1 + r2) on a ragged batch vs torch fp32 with
+    the torch-path Activation1d (oracle) rounded to bf16 as the kernel stages it.
+    Tolerance: |err| <= 2e-2 * conv(|act|, |W|) + 1e-2 * |ref| (bf16 act staging and output)."""
+    from indextts.utils.synthetic import kaiser_sinc_lowpass
+    from indextts.vocoder.bigvgan import _Conv, conv1d_taps
+    from oracle.bigvgan_oracle import activation1d
+    _hip, lib = _lib()
+    torch.manual_seed(C * k + d)
+    B, T = 3, 300
+    lens = torch.tensor([300, 57, 5], dtype=torch.int32)
+    x = torch.randn(B, T, C).to(torch.bfloat16)
+    res = [torch.randn(B, T, C).to(torch.bfloat16) for _ in range(nres)]
+    w = torch.randn(C, C, k) / (C * k) ** 0.5
+    bias = torch.randn(C) * 0.1
+    filt = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1)
+    la, lb = torch.randn(C) * 0.3, torch.randn(C) * 0.3
+    conv = _Conv(*conv1d_taps(w, d), bias, C, C, "cuda")
+    xd, lensd = x.cuda(), lens.cuda()
+    rd = [r.cuda() for r in res]
+    fd, lad, lbd = filt.cuda(), la.cuda(), lb.cuda()
+    y = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
+    _hip.check(lib.itts_amp_conv_fwd(
+        xd.data_ptr(), T * C, C, fd.data_ptr() if use_act else None, fd.data_ptr() if use_act else None,
+        lad.data_ptr() if use_act else None, lbd.data_ptr() if use_act else None, conv.w.data_ptr(),
+        conv.bias.data_ptr(), rd[0].data_ptr() if nres > 0 else None, rd[1].data_ptr() if nres > 1 else None,
+        y.data_ptr(), T * C, C, lensd.data_ptr(), B, T, C, C, conv.ntaps, conv.offs, alpha, _hip.stream_ptr()),
+        "amp_conv")
+    torch.cuda.synchronize()
+    wq = w.to(torch.bfloat16).float()
+    for b in range(B):
+        L = int(lens[b])
+        xb = x[b:b + 1, :L].float().transpose(1, 2)
+        if use_act:
+            xb = activation1d(xb, filt, filt, la, lb).to(torch.bfloat16).float()
+        ref = F.conv1d(xb, wq, bias, dilation=d, padding=d * (k - 1) // 2)[0].t()
+        for r in res:
+            ref = ref + r[b, :L].float()
+        ref = alpha * ref
+        scale = alpha * F.conv1d(xb.abs(), wq.abs(), dilation=d, padding=d * (k - 1) // 2)[0].t()
+        err = (y[b, :L].float().cpu() - ref).abs()
+        assert bool((err <= 2e-2 * scale + 1e-2 * ref.abs() + 1e-3).all()), (b, float(err.max()))
