@@ -38,7 +38,7 @@ __device__ __forceinline__ float snake(float u, float a, float inv_b) {
   return u + inv_b * (s * s);
 }
 
-template <typename TI, typename TO>
+template <typename TI, typename TO, bool VEC>
 __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
   extern __shared__ __attribute__((aligned(16))) float xs[];
   const int b = blockIdx.z;
@@ -51,11 +51,43 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
   TO* y = reinterpret_cast<TO*>(p.y) + (int64_t)b * p.syb;
 
   const int rows = TT + 2 * kHalo;
-  for (int idx = threadIdx.x; idx < rows * CT; idx += kThreads) {
-    int r = idx / CT, c = idx - r * CT;
-    int t = min(max(t0 - kHalo + r, 0), len - 1);
-    int ch = c0 + c;
-    xs[idx] = ch < p.C ? St<TI>::ld(x + (int64_t)t * p.sxt + (int64_t)ch * p.sxc) : 0.f;
+  if constexpr (VEC) {
+    // channel-last bf16 with C % 8 == 0: 16-B loads, every load of the tile issued before the
+    // first LDS write (one memory latency per block instead of one per loop trip)
+    constexpr int kMaxV = 3;  // vectors per thread: rows*CT/8 = (256/CT*16 + 12)*CT/8 <= 608 for CT <= 64
+    const int cv = CT / 8, nv = rows * cv;
+    u32x4_t buf[kMaxV];
+#pragma unroll
+    for (int i = 0; i < kMaxV; ++i) {
+      const int v = threadIdx.x + kThreads * i;
+      buf[i] = u32x4_t{0u, 0u, 0u, 0u};
+      if (v < nv) {
+        const int r = v / cv, c = (v - r * cv) * 8;
+        const int t = min(max(t0 - kHalo + r, 0), len - 1);
+        if (c0 + c < p.C)
+          buf[i] = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(x) + (int64_t)t * p.sxt + c0 + c);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxV; ++i) {
+      const int v = threadIdx.x + kThreads * i;
+      if (v < nv) {
+        const int r = v / cv, c = (v - r * cv) * 8;
+        float* d = xs + r * CT + c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          d[2 * e] = __uint_as_float(buf[i][e] << 16);
+          d[2 * e + 1] = __uint_as_float(buf[i][e] & 0xFFFF0000u);
+        }
+      }
+    }
+  } else {
+    for (int idx = threadIdx.x; idx < rows * CT; idx += kThreads) {
+      int r = idx / CT, c = idx - r * CT;
+      int t = min(max(t0 - kHalo + r, 0), len - 1);
+      int ch = c0 + c;
+      xs[idx] = ch < p.C ? St<TI>::ld(x + (int64_t)t * p.sxt + (int64_t)ch * p.sxc) : 0.f;
+    }
   }
   __syncthreads();
 
@@ -118,10 +150,13 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
 }
 
 template <typename TI, typename TO>
-void launch(const ActArgs& a, hipStream_t s) {
+void launch(const ActArgs& a, bool vec, hipStream_t s) {
   dim3 grid((a.T + a.nsub * kTO - 1) / (a.nsub * kTO), (a.C + a.CT - 1) / a.CT, a.B);
   size_t lds = sizeof(float) * (size_t)(a.nsub * kTO + 2 * kHalo) * a.CT;
-  hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO>), grid, dim3(kThreads), lds, s, a);
+  if (vec)
+    hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, true>), grid, dim3(kThreads), lds, s, a);
+  else
+    hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, false>), grid, dim3(kThreads), lds, s, a);
 }
 
 }  // namespace
@@ -140,10 +175,13 @@ extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, 
   a.CT = C < 64 ? C : 64;
   a.nsub = kThreads / a.CT;
   hipStream_t s = itts::as_stream(stream);
-  if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, s);
-  else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, s);
-  else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, s);
-  else launch<uint16_t, float>(a, s);
+  // vectorised staging: channel-last bf16 input, 16-B aligned rows
+  const bool vec = dtype_in == ITTS_BF16 && x_sc == 1 && C % 8 == 0 && x_st % 8 == 0 && x_sb % 8 == 0 &&
+                   (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, s);
+  else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, false, s);
+  else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, false, s);
+  else launch<uint16_t, float>(a, vec, s);
   return itts::check_launch(fn);
 }
 

@@ -75,21 +75,48 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
       *reinterpret_cast<u32x4_t*>(Aw + r * PA + c * 2) = u32x4_t{0u, 0u, 0u, 0u};
     }
   }
+  // every 16-B load of the window is issued before the first LDS write (one memory latency per
+  // block, not one per loop trip): at most kLV vectors per thread
+  constexpr int kLV = ((TT + kSpan + 12) * (CIN_PAD / 8) + 255) / 256;
+  u32x4_t lv[kLV];
   if (act) {  // rows replicate-clamped: the activation's own padding at the utterance edges
     const int XR = WR + 12;  // t = q0 - hl - 6 + r
     uint16_t* xr = reinterpret_cast<uint16_t*>(Xr);
-    for (int v = tid; v < XR * cv8; v += 256) {
-      const int r = v / cv8, c = (v - r * cv8) * 8;
-      const int t = min(max(q0 - p.hl - 6 + r, 0), len - 1);
-      *reinterpret_cast<u32x4_t*>(xr + r * Cin + c) = *reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c);
+#pragma unroll
+    for (int i = 0; i < kLV; ++i) {
+      const int v = tid + 256 * i;
+      if (v < XR * cv8) {
+        const int r = v / cv8, c = (v - r * cv8) * 8;
+        const int t = min(max(q0 - p.hl - 6 + r, 0), len - 1);
+        lv[i] = *reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kLV; ++i) {
+      const int v = tid + 256 * i;
+      if (v < XR * cv8) {
+        const int r = v / cv8, c = (v - r * cv8) * 8;
+        *reinterpret_cast<u32x4_t*>(xr + r * Cin + c) = lv[i];
+      }
     }
   } else {  // rows outside [0, len) are the conv's zero padding
-    for (int v = tid; v < WR * cv8; v += 256) {
-      const int r = v / cv8, c = (v - r * cv8) * 8;
-      const int t = q0 - p.hl + r;
-      u32x4_t val = {0u, 0u, 0u, 0u};
-      if (t >= 0 && t < len) val = *reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c);
-      *reinterpret_cast<u32x4_t*>(Aw + r * PA + c * 2) = val;
+#pragma unroll
+    for (int i = 0; i < kLV; ++i) {
+      const int v = tid + 256 * i;
+      lv[i] = u32x4_t{0u, 0u, 0u, 0u};
+      if (v < WR * cv8) {
+        const int r = v / cv8, c = (v - r * cv8) * 8;
+        const int t = q0 - p.hl + r;
+        if (t >= 0 && t < len) lv[i] = *reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kLV; ++i) {
+      const int v = tid + 256 * i;
+      if (v < WR * cv8) {
+        const int r = v / cv8, c = (v - r * cv8) * 8;
+        *reinterpret_cast<u32x4_t*>(Aw + r * PA + c * 2) = lv[i];
+      }
     }
   }
   __syncthreads();
@@ -159,6 +186,25 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
     __syncthreads();
   }
 
+  // residual rows of this tile: loads issued now, consumed in the epilogue (latency hidden by the MFMAs)
+  constexpr int kEV = (TT * COUT_PAD / 8 + 255) / 256;
+  const int rows = min(TT, len - q0);
+  const int nvec = rows * Cout / 8;
+  uint16_t* Y = p.y + (int64_t)b * p.syb + (int64_t)q0 * p.ldy;
+  const uint16_t* R1 = p.r1 ? p.r1 + (int64_t)b * p.syb + (int64_t)q0 * p.ldy : nullptr;
+  const uint16_t* R2 = p.r2 ? p.r2 + (int64_t)b * p.syb + (int64_t)q0 * p.ldy : nullptr;
+  u32x4_t rv1[kEV], rv2[kEV];
+#pragma unroll
+  for (int i = 0; i < kEV; ++i) {
+    const int v = tid + 256 * i;
+    if (v < nvec) {
+      const int e = v * 8, r = e / Cout, c = e - r * Cout;
+      const int64_t off = (int64_t)r * p.ldy + c;
+      if (R1) rv1[i] = *reinterpret_cast<const u32x4_t*>(R1 + off);
+      if (R2) rv2[i] = *reinterpret_cast<const u32x4_t*>(R2 + off);
+    }
+  }
+
   // ---- 3. MFMA over taps x K chunks; wave w owns output rows [32(w + 4i), +32), i < FM ----
   const int r32 = lane & 31, h = lane >> 5;
   f32x16_t acc[FM][FN];
@@ -214,36 +260,32 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
         Ys[(32 * (wave + 4 * i) + (r & 3) + 8 * (r >> 2) + 4 * h) * Cout + col] = acc[i][n][r];
     }
   __syncthreads();
-  const int rows = min(TT, len - q0);
-  const int nvec = rows * Cout / 8;
-  uint16_t* Y = p.y + (int64_t)b * p.syb + (int64_t)q0 * p.ldy;
-  const uint16_t* R1 = p.r1 ? p.r1 + (int64_t)b * p.syb + (int64_t)q0 * p.ldy : nullptr;
-  const uint16_t* R2 = p.r2 ? p.r2 + (int64_t)b * p.syb + (int64_t)q0 * p.ldy : nullptr;
-  for (int v = tid; v < nvec; v += 256) {
+#pragma unroll
+  for (int i = 0; i < kEV; ++i) {
+    const int v = tid + 256 * i;
+    if (v >= nvec) continue;
     const int e = v * 8, r = e / Cout, c = e - r * Cout;
     const int64_t off = (int64_t)r * p.ldy + c;
     float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = Ys[e + i] + p.bias[c + i];
+    for (int k = 0; k < 8; ++k) o[k] = Ys[e + k] + p.bias[c + k];
     if (R1) {
-      const u32x4_t rv = *reinterpret_cast<const u32x4_t*>(R1 + off);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        o[2 * i] += __uint_as_float(rv[i] << 16);
-        o[2 * i + 1] += __uint_as_float(rv[i] & 0xFFFF0000u);
+      for (int k = 0; k < 4; ++k) {
+        o[2 * k] += __uint_as_float(rv1[i][k] << 16);
+        o[2 * k + 1] += __uint_as_float(rv1[i][k] & 0xFFFF0000u);
       }
     }
     if (R2) {
-      const u32x4_t rv = *reinterpret_cast<const u32x4_t*>(R2 + off);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        o[2 * i] += __uint_as_float(rv[i] << 16);
-        o[2 * i + 1] += __uint_as_float(rv[i] & 0xFFFF0000u);
+      for (int k = 0; k < 4; ++k) {
+        o[2 * k] += __uint_as_float(rv2[i][k] << 16);
+        o[2 * k + 1] += __uint_as_float(rv2[i][k] & 0xFFFF0000u);
       }
     }
     u32x4_t out;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = pack2bf(p.alpha * o[2 * i], p.alpha * o[2 * i + 1]);
+    for (int k = 0; k < 4; ++k) out[k] = pack2bf(p.alpha * o[2 * k], p.alpha * o[2 * k + 1]);
     *reinterpret_cast<u32x4_t*>(Y + off) = out;
   }
 }
