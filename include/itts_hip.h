@@ -107,9 +107,12 @@ int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed, int K, in
 /* One decode step of 16x64 causal attention per row: appends this step's k/v at position
  * kv_base + tstate[0] of the cache [B][H][smax][64] and attends over the valid (pad-masked,
  * quirk Q2) prefix.  HF modeling_gpt2.py:54-72,185-225 with the additive padding mask. */
-int itts_attn_decode(const float* qkv, int64_t ldqkv, void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs,
-                     int smax, const int32_t* pad, int kv_base, const int32_t* tstate, void* out, int64_t ldo, int B,
-                     int H, int cache_dtype, int out_dtype, void* stream);
+/* q/k/v = qkv_bias (nullable) + sum of `nsplit` slabs qkv + s*split_stride (split-K partials of
+ * c_attn, so that GEMM needs no reduce pass; nsplit = 1 with a finished qkv row is the plain case). */
+int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride, const float* qkv_bias,
+                     void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs, int smax, const int32_t* pad,
+                     int kv_base, const int32_t* tstate, void* out, int64_t ldo, int B, int H, int cache_dtype,
+                     int out_dtype, void* stream);
 /* Causal attention over packed variable-length sequences (prefill and latent pass); optionally
  * writes K/V into the decode cache.  seq_pad[b] leading rows are masked (left padding, Q2). */
 int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start, const int32_t* seq_len,

@@ -7,7 +7,8 @@
 //    over keys [pad_b, kv_base + *t].  One 256-thread workgroup per (head, sequence), ONE pass over
 //    the cache: 8 lanes per key row (one 1 KiB coalesced wave load = 8 rows of K, one of V), online
 //    softmax per 8-lane group, log-sum-exp merge of the 32 groups through LDS.  HBM-bound: it
-//    streams 2 * S * 64 * sizeof(cache) bytes per (sequence, head).
+//    streams 2 * S * 64 * sizeof(cache) bytes per (sequence, head).  The c_attn output may arrive
+//    as split-K partial slabs (summed here with the bias, so the GEMM needs no reduce pass).
 // 2. itts_attn_prefill: variable-length causal attention over packed sequences (prefill of the
 //    prompt block, and the teacher-forced latent pass).  One thread per query, K/V staged through
 //    LDS in 32-key blocks, block-wise online softmax; optionally writes K/V into the decode cache.
@@ -36,48 +37,60 @@ __device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]
 
 constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is the caller's
 
-template <typename TC, typename TO>
-__global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv,
-                                                          TC* __restrict__ cache_k, TC* __restrict__ cache_v,
-                                                          int64_t cache_bs, int64_t cache_hs, const int32_t* pad,
-                                                          int kv_base, const int32_t* __restrict__ tstate,
-                                                          TO* __restrict__ out, int64_t ldo, int H) {
+// One workgroup of NT threads per (head, sequence): NT/8 groups of 8 lanes, group g owns keys
+// g, g + NT/8, ...; lane d8 holds dims 8*d8 .. 8*d8+7.  Single pass: the K and V rows of KB keys
+// per group are loaded together (all loads of a round in flight), scores via 8-lane shuffles, an
+// online softmax per group (running max m, sum l, partial output o); groups merge through LDS.
+// (Measured on MI355X at B=32, S~283: NT = 256 beats 512-thread workgroups, and beats issuing the
+// cache loads before the q/k/v summation with 16 packed keys per group -- 308 VGPRs, 1 wave/SIMD.)
+// q/k/v = bias + sum of `nsplit` split-K partial slabs of the c_attn GEMM (stride split_stride).
+template <typename TC, typename TO, int NT>
+__global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
+                                                         int64_t split_stride, const float* __restrict__ qkv_bias,
+                                                         TC* __restrict__ cache_k, TC* __restrict__ cache_v,
+                                                         int64_t cache_bs, int64_t cache_hs, const int32_t* pad,
+                                                         int kv_base, const int32_t* __restrict__ tstate,
+                                                         TO* __restrict__ out, int64_t ldo, int H) {
+  constexpr int NG = NT / 8;
+  constexpr int KB = 8;
   __shared__ float qs[kHD], kn[kHD], vn[kHD];
-  __shared__ float gm[32], gl[32];
-  __shared__ float pv[32][kHD + 1];
+  __shared__ float gm[NG], gl[NG];
+  __shared__ float pv[NG][kHD + 1];
   const int h = blockIdx.x, b = blockIdx.y;
   const int D = H * kHD;
   const int kidx = kv_base + tstate[0];
   const int p0 = pad ? pad[b] : 0;
   const int nk = kidx + 1 - p0;
-  const float* row = qkv + (int64_t)b * ldqkv + h * kHD;
   TC* Kc = cache_k + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
   TC* Vc = cache_v + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
-  if (threadIdx.x < kHD) {
-    const int d = threadIdx.x;
-    qs[d] = row[d] * 0.125f;  // 1/sqrt(64), exact
-    const float k = row[D + d], v = row[2 * D + d];
-    kn[d] = k;
-    vn[d] = v;
-    St<TC>::st(Kc + (int64_t)kidx * kHD + d, k);
-    St<TC>::st(Vc + (int64_t)kidx * kHD + d, v);
+  if (threadIdx.x < 3 * kHD) {
+    const int part = threadIdx.x / kHD, d = threadIdx.x - part * kHD;  // 0: q, 1: k, 2: v
+    const int col = part * D + h * kHD + d;
+    const float* src = qkv + (int64_t)b * ldqkv + col;
+    float v = qkv_bias ? qkv_bias[col] : 0.f;
+    for (int s = 0; s < nsplit; ++s) v += src[s * split_stride];
+    if (part == 0) {
+      qs[d] = v * 0.125f;  // 1/sqrt(64), exact
+    } else if (part == 1) {
+      kn[d] = v;
+      St<TC>::st(Kc + (int64_t)kidx * kHD + d, v);
+    } else {
+      vn[d] = v;
+      St<TC>::st(Vc + (int64_t)kidx * kHD + d, v);
+    }
   }
   __syncthreads();
-  // 32 groups of 8 lanes; group g owns keys g, g+32, ...; lane d8 holds dims 8*d8 .. 8*d8+7.
-  // Single pass: K and V rows of KB keys are loaded together, scores via 8-lane shuffles, and an
-  // online softmax per group (running max m, sum l, partial output o); groups merge through LDS.
   const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
   float q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) q[e] = qs[8 * d8 + e];
-  constexpr int KB = 8;
   float m = -INFINITY, l = 0.f;
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 0; j0 < nk; j0 += 32 * KB) {
+  for (int j0 = 0; j0 < nk; j0 += NG * KB) {
     float k[KB][8], v[KB][8];
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
-      const int j = j0 + 32 * u + g;
+      const int j = j0 + NG * u + g;
       if (j < nk && p0 + j != kidx) {
         load8<TC>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8, k[u]);
         load8<TC>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8, v[u]);
@@ -99,7 +112,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
       part += __shfl_xor(part, 1, 64);
       part += __shfl_xor(part, 2, 64);
       part += __shfl_xor(part, 4, 64);
-      s[u] = (j0 + 32 * u + g < nk) ? part : -INFINITY;
+      s[u] = (j0 + NG * u + g < nk) ? part : -INFINITY;
       bm = fmaxf(bm, s[u]);
     }
     if (bm == -INFINITY) continue;  // this group has no valid key in the round
@@ -110,10 +123,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
     for (int e = 0; e < 8; ++e) o[e] *= corr;
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
-      const float p = __expf(s[u] - mn);
-      l += p;
+      const float pr = __expf(s[u] - mn);
+      l += pr;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = fmaf(p, v[u][e], o[e]);
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(pr, v[u][e], o[e]);
     }
     m = mn;
   }
@@ -127,10 +140,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const float* __restric
   if (threadIdx.x < kHD) {
     float M = -INFINITY;
 #pragma unroll 8
-    for (int i = 0; i < 32; ++i) M = fmaxf(M, gm[i]);
+    for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
     float L = 0.f, acc = 0.f;
 #pragma unroll 8
-    for (int i = 0; i < 32; ++i) {
+    for (int i = 0; i < NG; ++i) {
       const float w = __expf(gm[i] - M);  // empty group: exp(-inf) = 0
       L = fmaf(gl[i], w, L);
       acc = fmaf(pv[i][threadIdx.x], w, acc);
@@ -219,19 +232,20 @@ __global__ __launch_bounds__(kQB) void attn_prefill_kernel(const float* __restri
 
 }  // namespace
 
-extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, void* cache_k, void* cache_v, int64_t cache_bs,
+extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
+                                const float* qkv_bias, void* cache_k, void* cache_v, int64_t cache_bs,
                                 int64_t cache_hs, int smax, const int32_t* pad, int kv_base, const int32_t* tstate,
                                 void* out, int64_t ldo, int B, int H, int cache_dtype, int out_dtype, void* stream) {
   const char* fn = "itts_attn_decode";
-  ITTS_REQUIRE(B >= 0 && H > 0, fn, "bad sizes");
+  ITTS_REQUIRE(B >= 0 && H > 0 && nsplit >= 1, fn, "bad sizes");
   if (B == 0) return 0;
   ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && out, fn, "null pointer");
   ITTS_REQUIRE(smax <= kMaxKeys && cache_hs >= (int64_t)smax * kHD, fn, "bad cache capacity");
   dim3 grid(H, B);
   hipStream_t s = itts::as_stream(stream);
-#define ITTS_AD(TC, TO)                                                                                          \
-  hipLaunchKernelGGL((attn_decode_kernel<TC, TO>), grid, dim3(256), 0, s, qkv, ldqkv, (TC*)cache_k, (TC*)cache_v, \
-                     cache_bs, cache_hs, pad, kv_base, tstate, (TO*)out, ldo, H)
+#define ITTS_AD(TC, TO)                                                                                             \
+  hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit, split_stride,    \
+                     qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base, tstate, (TO*)out, ldo, H)
   if (cache_dtype == ITTS_BF16 && out_dtype == ITTS_BF16) ITTS_AD(uint16_t, uint16_t);
   else if (cache_dtype == ITTS_F32 && out_dtype == ITTS_F32) ITTS_AD(float, float);
   else if (cache_dtype == ITTS_BF16) ITTS_AD(uint16_t, float);

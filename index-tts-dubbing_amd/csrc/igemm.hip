@@ -14,7 +14,8 @@
 //
 // Tiling: 256 threads = 4 waves; block tile TM x TN, K step KC (channels of one tap) staged
 // through double-buffered LDS (row pitch padded by 16 B -> conflict-free ds_read_b128 fragments),
-// next K-step's global loads issued into registers before the current step's MFMAs.
+// with a 3-deep register ring (K-step it+2's global loads in flight while step it computes).
+// Tiles are remapped XCD-aware (output-channel tiles of one row tile run together on one XCD).
 #include "common.h"
 
 namespace {
@@ -54,19 +55,31 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
   constexpr int WAVES_N = TN / WN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-  const int b = blockIdx.z;
+  // XCD-aware tile order (guide T1): dispatch places block p on XCD p % 8, so a bijective remap
+  // gives every XCD a contiguous run of logical tiles, ordered N-tile fastest -- the blocks that share
+  // an input window (same rows, different output channels) run together on one XCD and hit its L2.
+  const int ntn = (p.Cout + TN - 1) / TN, ntm = (p.Tmax + TM - 1) / TM;
+  const int nblk = ntn * ntm * p.B;
+  const int pid = blockIdx.x, xcd = pid % 8, qn = nblk / 8, rn = nblk % 8;
+  const int lid = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + pid / 8;
+  const int b = lid / (ntn * ntm);
   const int len = p.lens ? p.lens[b] : p.Tmax;
-  const int q0 = blockIdx.x * TM;
+  const int q0 = ((lid / ntn) % ntm) * TM;
   if (q0 >= len) return;
-  const int n0 = blockIdx.y * TN;
+  const int n0 = (lid % ntn) * TN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
   const uint16_t* X = p.x + (int64_t)b * p.sxb;
   const int nchunks = p.ci_pad / KC;
   const int kiters = p.ntaps * nchunks;
 
-  u32x4_t ra[A_VEC], rb[B_VEC];
-  auto gload = [&](int it) {
+  // 3-deep register ring: the global loads of K-step it+2 are issued while step it computes, so
+  // every load has two steps of MFMAs (plus the other block's) to arrive before its LDS write.
+  struct Stage {
+    u32x4_t a[A_VEC], b[B_VEC];
+  };
+  Stage S0, S1, S2;
+  auto gload = [&](int it, Stage& r) {
     const int j = it / nchunks, c0 = (it - j * nchunks) * KC;
     const int toff = p.tap_off[j];
 #pragma unroll
@@ -85,27 +98,27 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
           val = u32x4_t{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
         }
       }
-      ra[i] = val;
+      r.a[i] = val;
     }
     const uint16_t* Wj = p.w + ((int64_t)j * p.co_pad + n0) * p.ci_pad + c0;
 #pragma unroll
     for (int i = 0; i < B_VEC; ++i) {
       const int v = tid + 256 * i, row = v / VPR, cv = (v % VPR) * 8;
-      if (v < B_TOT) rb[i] = *reinterpret_cast<const u32x4_t*>(Wj + (int64_t)row * p.ci_pad + cv);
+      if (v < B_TOT) r.b[i] = *reinterpret_cast<const u32x4_t*>(Wj + (int64_t)row * p.ci_pad + cv);
     }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](int buf, const Stage& r) {
     unsigned char* As = smem + buf * (A_BYTES + B_BYTES);
     unsigned char* Bs = As + A_BYTES;
 #pragma unroll
     for (int i = 0; i < A_VEC; ++i) {
       const int v = tid + 256 * i, row = v / VPR, cv = v % VPR;
-      if (v < A_TOT) *reinterpret_cast<u32x4_t*>(As + row * PITCH + cv * 16) = ra[i];
+      if (v < A_TOT) *reinterpret_cast<u32x4_t*>(As + row * PITCH + cv * 16) = r.a[i];
     }
 #pragma unroll
     for (int i = 0; i < B_VEC; ++i) {
       const int v = tid + 256 * i, row = v / VPR, cv = v % VPR;
-      if (v < B_TOT) *reinterpret_cast<u32x4_t*>(Bs + row * PITCH + cv * 16) = rb[i];
+      if (v < B_TOT) *reinterpret_cast<u32x4_t*>(Bs + row * PITCH + cv * 16) = r.b[i];
     }
   };
 
@@ -118,12 +131,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int r32 = lane & 31, h = lane >> 5;
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  for (int it = 0; it < kiters; ++it) {
-    const int buf = it & 1;
-    if (it + 1 < kiters) gload(it + 1);
+  auto compute = [&](int buf) {
     const unsigned char* As = smem + buf * (A_BYTES + B_BYTES);
     const unsigned char* Bs = As + A_BYTES;
 #pragma unroll
@@ -140,10 +148,25 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  };
+  // step it: issue loads for it+2 into `ld`, compute LDS buffer it&1, write stage it+1 (`wr`) into
+  // the other buffer (last read in step it-1, fenced by that step's barrier), barrier
+  auto step = [&](int it, Stage& ld, const Stage& wr) {
+    if (it + 2 < kiters) gload(it + 2, ld);
+    compute(it & 1);
     if (it + 1 < kiters) {
-      swrite(buf ^ 1);
+      swrite((it + 1) & 1, wr);
       __syncthreads();
     }
+  };
+  gload(0, S0);
+  if (kiters > 1) gload(1, S1);
+  swrite(0, S0);
+  __syncthreads();
+  for (int it = 0; it < kiters; it += 3) {
+    step(it, S2, S1);
+    if (it + 1 < kiters) step(it + 1, S0, S2);
+    if (it + 2 < kiters) step(it + 2, S1, S0);
   }
 
   // epilogue: lane holds column n = wn + 32j + (lane&31); rows (r&3) + 8(r>>2) + 4h
@@ -177,7 +200,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
 
 template <int TM, int TN, int WM, int WN, int KC, typename OutT>
 void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
-  dim3 grid((a.Tmax + TM - 1) / TM, (a.Cout + TN - 1) / TN, a.B);
+  dim3 grid(((a.Tmax + TM - 1) / TM) * ((a.Cout + TN - 1) / TN) * a.B);
   size_t lds = 2 * (size_t)(TM + TN) * (KC * 2 + 16);
   if (vec)
     hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT>), grid, dim3(256), lds, s, a);

@@ -45,7 +45,8 @@ SIGNATURES = {
     "itts_residual_reduce_ln": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp,
                                        _vp, _vp, _c_i, _vp]),
     "itts_gemm_f32": (_c_i, [_vp, _c_i64, _vp, _c_i64, _c_i, _c_i, _c_i, _vp, _c_i, _vp, _vp, _c_i64, _vp]),
-    "itts_attn_decode": (_c_i, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_i, _vp, _c_i, _vp, _vp, _c_i64, _c_i, _c_i,
+    "itts_attn_decode": (_c_i, [_vp, _c_i64, _c_i, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _c_i, _vp, _c_i, _vp, _vp,
+                                _c_i64, _c_i, _c_i,
                                 _c_i, _c_i, _vp]),
     "itts_attn_prefill": (_c_i, [_vp, _c_i64, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i,
                                  _c_i, _c_i, _vp]),

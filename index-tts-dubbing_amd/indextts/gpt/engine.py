@@ -196,7 +196,7 @@ class HipGPT:
             "B": B, "Mp": Mp, "max_new": max_new,
             "x": torch.zeros(B, D, device=dev),
             "h": torch.zeros(Mp, D, dtype=ad, device=dev),
-            "qkv": torch.zeros(B, 3 * D, device=dev),
+            "qkv": torch.zeros(self.KSPLIT["qkv"] * B * 3 * D, device=dev),  # c_attn split-K slabs [split][B][3D]
             "o": torch.zeros(Mp, D, dtype=ad, device=dev),
             "f": torch.zeros(Mp, 4 * D, dtype=ad, device=dev),
             "ws": torch.zeros(8 * B * D, device=dev),  # split-K partial products [split][B][D]
@@ -237,14 +237,17 @@ class HipGPT:
         x, h, qkv, o, f = st["x"], st["h"], st["qkv"], st["o"], st["f"]
         for li, ly in enumerate(self.layers):
             if self.mode == "f32":
-                self._gemm(h[:B], ly.w["qkv"], qkv, bias=ly.b["qkv"])
-            else:  # h = ln_1(x) was produced by the previous reduce (or the sampler for layer 0)
-                self._dg(h, ly.w["qkv"], B, ly.b["qkv"], qkv)
+                self._gemm(h[:B], ly.w["qkv"], qkv[: B * 3 * D].view(B, 3 * D), bias=ly.b["qkv"])
+                kq, qkv_bias = 1, None
+            else:  # h = ln_1(x) was produced by the previous reduce (or the sampler for layer 0);
+                # c_attn as split-K slabs, summed (+ bias) by the attention kernel
+                kq, qkv_bias = self._ksplit(ly.w["qkv"]["K"], self.KSPLIT["qkv"]), ly.b["qkv"]
+                self._dg(h, ly.w["qkv"], B, None, qkv, epi=2, ksplit=kq)
             kc, vc = st["kc"][li], st["vc"][li]
             _hip.check(self.lib.itts_attn_decode(
-                qkv.data_ptr(), 3 * D, kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1), self.max_kv,
-                st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(), o.data_ptr(), D, B, self.H,
-                _hip.dtype_code(kc), _hip.dtype_code(o), stream), "itts_attn_decode")
+                qkv.data_ptr(), 3 * D, kq, B * 3 * D, _hip.ptr(qkv_bias), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+                kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(), o.data_ptr(), D, B,
+                self.H, _hip.dtype_code(kc), _hip.dtype_code(o), stream), "itts_attn_decode")
             nxt = self.layers[li + 1].ln1 if li + 1 < self.L else None
             if self.mode == "f32":
                 self._gemm(o[:B], ly.w["o"], x, bias=ly.b["o"], residual=True)
@@ -274,7 +277,7 @@ class HipGPT:
         _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
     # split-K factors of the residual projections (partials reduced by itts_residual_reduce_ln)
-    KSPLIT = {"o": 2, "proj": 8}
+    KSPLIT = {"qkv": 2, "o": 2, "proj": 8}
 
     @staticmethod
     def _ksplit(K, want):

@@ -98,11 +98,12 @@ def test_residual_reduce_ln_matches_torch():
     torch.testing.assert_close(h.float().cpu(), hr, rtol=1e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("S,cache", [(1, "bf16"), (37, "bf16"), (300, "bf16"), (1000, "bf16"), (300, "f32")])
-def test_attn_decode_matches_torch(S, cache):
-    """One decode step: appends k/v at kv_base + t, then softmax(q k^T / 8 + pad mask) v over the
-    cached prefix; vs torch fp32 on the same (cache-rounded) keys/values.  |err| <= 2e-3 (bf16
-    output rounding) / 1e-5 (f32)."""
+@pytest.mark.parametrize("S,cache,nsplit", [(1, "bf16", 1), (37, "bf16", 3), (300, "bf16", 4), (1000, "bf16", 1),
+                                            (300, "f32", 1), (513, "bf16", 2)])
+def test_attn_decode_matches_torch(S, cache, nsplit):
+    """One decode step: q/k/v = bias + sum of nsplit c_attn partial slabs; appends k/v at
+    kv_base + t, then softmax(q k^T / 8 + pad mask) v over the cached prefix; vs torch fp32 on the
+    same (cache-rounded) keys/values.  |err| <= 2e-2 (bf16 output rounding) / 1e-5 (f32)."""
     _hip, lib = _lib()
     torch.manual_seed(S)
     B, H, smax = 5, 16, S + 8
@@ -110,14 +111,20 @@ def test_attn_decode_matches_torch(S, cache):
     cdt = torch.bfloat16 if cache == "bf16" else torch.float32
     kc = (torch.randn(B, H, smax, 64) * 0.5).to(cdt)
     vc = torch.randn(B, H, smax, 64).to(cdt)
-    qkv = torch.randn(B, 3 * D)
+    parts = torch.randn(nsplit, B, 3 * D) / nsplit ** 0.5
+    bias = torch.randn(3 * D) * 0.1 if nsplit > 1 else None
+    qkv = bias.expand(B, -1).clone() if bias is not None else torch.zeros(B, 3 * D)
+    for sp in range(nsplit):  # the kernel's summation order (bias first), so k/v rows compare exactly
+        qkv = qkv + parts[sp]
     pad = torch.tensor([0, 3, 0, min(7, S - 1), 1], dtype=torch.int32).clamp(max=S - 1)
     kv_base, t = S - 1 - 2, 2  # new key lands at index S - 1
     kd, vd = kc.clone().cuda(), vc.clone().cuda()
     out = torch.zeros(B, D, dtype=cdt).cuda()
     tst = torch.tensor([t, 0, 0, 0], dtype=torch.int32).cuda()
-    qkv_d, pad_d = qkv.cuda(), pad.cuda()  # keep device temporaries alive until the kernel ran
-    _hip.check(lib.itts_attn_decode(qkv_d.data_ptr(), 3 * D, kd.data_ptr(), vd.data_ptr(), kd.stride(0),
+    qkv_d, pad_d = parts.cuda(), pad.cuda()  # keep device temporaries alive until the kernel ran
+    bias_d = bias.cuda() if bias is not None else None
+    _hip.check(lib.itts_attn_decode(qkv_d.data_ptr(), 3 * D, nsplit, B * 3 * D, _hip.ptr(bias_d), kd.data_ptr(),
+                                    vd.data_ptr(), kd.stride(0),
                                     kd.stride(1), smax, pad_d.data_ptr(), kv_base, tst.data_ptr(),
                                     out.data_ptr(), D, B, H, _hip.dtype_code(kd), _hip.dtype_code(out),
                                     _hip.stream_ptr()), "attn_decode")
