@@ -122,7 +122,9 @@ int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start,
  * RepetitionPenalty over all seen ids incl. the fake prefix ids (Q4; HF logits_process.py:409-412),
  * min_new_tokens, first-index argmax (HF generation/utils.py:2894-2925), finished rows -> stop,
  * x = mel_embedding(tok) + mel_pos[col + pos_delta] (Q1, gpt/model.py:151-155), h = ln_1(x).
- * col = tstate[0] + col_delta (device counter: graph-replayable).  forced (tests): feed these ids. */
+ * col = tstate[0] + col_delta (device counter: graph-replayable).  forced (tests): feed these ids.
+ * logits [B][ldl] f32 and seen [B][ldl] u8 share the row pitch ldl >= V (ldl % 4 == 0 with 16-B
+ * aligned rows takes the vectorised path). */
 int itts_sample_embed(const float* logits, int64_t ldl, int V, uint8_t* seen, uint8_t* done, int32_t* codes,
                       int64_t ldc, const int32_t* tstate, int col_delta, int min_new, int stop, float penalty,
                       const float* emb, const float* pos_emb, int pos_delta, int D, const float* ln_g,

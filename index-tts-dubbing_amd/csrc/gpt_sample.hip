@@ -148,7 +148,7 @@ __device__ __forceinline__ float processed_score(const SampleArgs& p, const floa
   return s;
 }
 
-template <typename TH>
+template <typename TH, bool VEC4>
 __global__ __launch_bounds__(kT) void sample_embed_kernel(SampleArgs p) {
   __shared__ float rv[kT / 64];
   __shared__ int ri[kT / 64];
@@ -156,14 +156,51 @@ __global__ __launch_bounds__(kT) void sample_embed_kernel(SampleArgs p) {
   const int b = blockIdx.x;
   const int col = p.tstate[0] + p.col_delta;
   const float* lr = p.logits + (int64_t)b * p.ldl;
-  uint8_t* sr = p.seen + (int64_t)b * p.V;
+  uint8_t* sr = p.seen + (int64_t)b * p.ldl;
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int v = threadIdx.x; v < p.V; v += kT) {
-    const float s = processed_score(p, lr, sr, v, col);
-    if (better(s, v, best, bi)) {
-      best = s;
-      bi = v;
+  if constexpr (VEC4) {
+    // 16-B logits + 4-B seen-flag loads, a whole row's loads in flight per thread (kI per trip)
+    constexpr int kI = 9;  // ceil(ceil(8194 / 4) / 256): the IndexTTS mel vocabulary in one trip
+    const int nv4 = (p.V + 3) >> 2;
+    const f32x4_t* l4 = reinterpret_cast<const f32x4_t*>(lr);
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(sr);
+    for (int base = 0; base < nv4; base += kT * kI) {
+      f32x4_t lv[kI];
+      uint32_t sv[kI];
+#pragma unroll
+      for (int i = 0; i < kI; ++i) {
+        const int idx = base + threadIdx.x + kT * i;
+        if (idx < nv4) {
+          lv[i] = l4[idx];
+          sv[i] = s4[idx];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kI; ++i) {
+        const int idx = base + threadIdx.x + kT * i;
+        if (idx >= nv4) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int v = 4 * idx + e;
+          if (v >= p.V) continue;
+          float s = lv[i][e];
+          if ((sv[i] >> (8 * e)) & 0xFFu) s = s < 0.f ? s * p.penalty : s / p.penalty;
+          if (v == p.stop && col < p.min_new) s = -INFINITY;
+          if (better(s, v, best, bi)) {
+            best = s;
+            bi = v;
+          }
+        }
+      }
+    }
+  } else {
+    for (int v = threadIdx.x; v < p.V; v += kT) {
+      const float s = processed_score(p, lr, sr, v, col);
+      if (better(s, v, best, bi)) {
+        best = s;
+        bi = v;
+      }
     }
   }
   block_argmax(best, bi, rv, ri);
@@ -189,7 +226,7 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
   const uint64_t row = (uint64_t)(uint32_t)(b + p.tstate[1]);  // tstate[1]: global index of row 0
   const uint64_t key = mix64(seed ^ mix64((row << 32) | (uint32_t)col));
   const float* lr = p.logits + (int64_t)b * p.ldl;
-  uint8_t* sr = p.seen + (int64_t)b * p.V;
+  uint8_t* sr = p.seen + (int64_t)b * p.ldl;
   float best = -INFINITY;
   int bi = 0x7fffffff;
   if (p.top_k <= 0) {  // plain multinomial == argmax(score + Gumbel noise)
@@ -293,11 +330,17 @@ int launch_sample(const char* fn, SampleArgs& p, int h_dtype, int B, bool do_sam
   ITTS_REQUIRE(!p.x || (p.emb && p.pos_emb), fn, "embedding output needs the embedding tables");
   ITTS_REQUIRE(!p.h || (p.x && p.g && p.bta), fn, "h output needs x and ln_1 params");
   hipStream_t s = itts::as_stream(stream);
+  ITTS_REQUIRE(p.ldl >= p.V, fn, "row pitch ldl < V");
   if (!do_sample) {
-    if (h_dtype == ITTS_BF16)
-      hipLaunchKernelGGL(sample_embed_kernel<uint16_t>, dim3(B), dim3(kT), 0, s, p);
+    const bool vec = p.ldl % 4 == 0 && ((reinterpret_cast<uintptr_t>(p.logits) | reinterpret_cast<uintptr_t>(p.seen)) & 15) == 0;
+    if (h_dtype == ITTS_BF16 && vec)
+      hipLaunchKernelGGL((sample_embed_kernel<uint16_t, true>), dim3(B), dim3(kT), 0, s, p);
+    else if (h_dtype == ITTS_BF16)
+      hipLaunchKernelGGL((sample_embed_kernel<uint16_t, false>), dim3(B), dim3(kT), 0, s, p);
+    else if (vec)
+      hipLaunchKernelGGL((sample_embed_kernel<float, true>), dim3(B), dim3(kT), 0, s, p);
     else
-      hipLaunchKernelGGL(sample_embed_kernel<float>, dim3(B), dim3(kT), 0, s, p);
+      hipLaunchKernelGGL((sample_embed_kernel<float, false>), dim3(B), dim3(kT), 0, s, p);
   } else {
     ITTS_REQUIRE(p.top_k >= 0 && p.top_k <= kMaxK, fn, "top_k must be in [0, 64]");
     ITTS_REQUIRE(p.top_k > 0 || p.top_p >= 1.f, fn, "top_p < 1 needs 0 < top_k <= 64");

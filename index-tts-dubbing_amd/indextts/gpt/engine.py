@@ -56,6 +56,7 @@ class HipGPT:
         self.D, self.L, self.H = int(g.model_dim), int(g.layers), int(g.heads)
         assert self.D == 64 * self.H, "kernels assume head size 64"
         self.V = int(g.number_mel_codes)
+        self.Vp = (self.V + 15) // 16 * 16  # logits / seen-flag row pitch (vectorised sampler loads)
         self.start_text, self.stop_text = int(g.start_text_token), int(g.stop_text_token)
         self.start_mel, self.stop_mel = int(g.start_mel_token), int(g.stop_mel_token)
         self.max_kv = int(max_kv or (32 + int(g.max_text_tokens) + 2 + 1 + int(g.max_mel_tokens)))
@@ -200,10 +201,10 @@ class HipGPT:
             "o": torch.zeros(Mp, D, dtype=ad, device=dev),
             "f": torch.zeros(Mp, 4 * D, dtype=ad, device=dev),
             "ws": torch.zeros(8 * B * D, device=dev),  # split-K partial products [split][B][D]
-            "logits": torch.zeros(B, self.V, device=dev),
+            "logits": torch.zeros(B, self.Vp, device=dev),  # row pitch Vp (16-B aligned rows)
             "kc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
             "vc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
-            "seen": torch.zeros(B, self.V, dtype=torch.uint8, device=dev),
+            "seen": torch.zeros(B, self.Vp, dtype=torch.uint8, device=dev),  # same row pitch as logits
             "done": torch.zeros(B, dtype=torch.uint8, device=dev),
             "codes": torch.full((B, max_new), self.stop_mel, dtype=torch.int32, device=dev),
             "t": torch.zeros(4, dtype=torch.int32, device=dev),
@@ -215,7 +216,7 @@ class HipGPT:
         smp = st.get("sampling")
         if smp is not None:  # (temperature, top_k, top_p); the seed is device state (t[2:4])
             _hip.check(self.lib.itts_sample_topk_embed(
-                st["logits"].data_ptr(), self.V, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
+                st["logits"].data_ptr(), self.Vp, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
                 st["codes"].data_ptr(), st["max_new"], st["t"].data_ptr(), col_delta, int(min_new), self.stop_mel,
                 float(penalty), float(smp[0]), int(smp[1]), float(smp[2]), self.mel_emb.data_ptr(),
                 self.mel_pos.data_ptr(), 2, self.D, self.layers[0].ln1[0].data_ptr(), self.layers[0].ln1[1].data_ptr(),
@@ -223,7 +224,7 @@ class HipGPT:
                 _hip.ptr(st.get("forced")), _hip.stream_ptr()), "itts_sample_topk_embed")
             return
         _hip.check(self.lib.itts_sample_embed(
-            st["logits"].data_ptr(), self.V, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
+            st["logits"].data_ptr(), self.Vp, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
             st["codes"].data_ptr(), st["max_new"], st["t"].data_ptr(), col_delta, int(min_new), self.stop_mel,
             float(penalty), self.mel_emb.data_ptr(), self.mel_pos.data_ptr(), 2, self.D,
             self.layers[0].ln1[0].data_ptr(), self.layers[0].ln1[1].data_ptr(), st["x"].data_ptr(),
