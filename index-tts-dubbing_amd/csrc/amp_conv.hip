@@ -48,7 +48,7 @@ __device__ __forceinline__ float snake_f(float u, float a, float inv_b) {
 
 __device__ __forceinline__ float ld_bf(const uint16_t* p) { return __uint_as_float(((uint32_t)*p) << 16); }
 
-template <int CIN_PAD, int COUT_PAD, int TT>
+template <int CIN_PAD, int COUT_PAD, int TT, bool ACT>
 __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   constexpr int PA = CIN_PAD * 2 + 16;  // activated-window row pitch (bytes)
   constexpr int FN = COUT_PAD / 32, KS = CIN_PAD / 16, FM = TT / 128;
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Cin = p.Cin, Cout = p.Cout;
   const int WR = TT + p.hl + p.hr;  // activated window rows: t = q0 - hl + r
-  const bool act = p.log_alpha != nullptr;
+  constexpr bool act = ACT;  // compile-time: the no-activation variant keeps its registers for the conv
   const uint16_t* X = p.x + (int64_t)b * p.sxb;
   unsigned char* Aw = smem;                         // [WR][PA]
   unsigned char* Xr = smem + (TT + kSpan) * PA;     // raw window / output tile
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   // block, not one per loop trip): at most kLV vectors per thread
   constexpr int kLV = ((TT + kSpan + 12) * (CIN_PAD / 8) + 255) / 256;
   u32x4_t lv[kLV];
-  if (act) {  // rows replicate-clamped: the activation's own padding at the utterance edges
+  if constexpr (ACT) {  // rows replicate-clamped: the activation's own padding at the utterance edges
     const int XR = WR + 12;  // t = q0 - hl - 6 + r
     uint16_t* xr = reinterpret_cast<uint16_t*>(Xr);
 #pragma unroll
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   __syncthreads();
 
   // ---- 2. activation: work item = 16 consecutive rows of one channel (register window) ----
-  if (act) {
+  if constexpr (ACT) {
     const uint16_t* xr = reinterpret_cast<const uint16_t*>(Xr);
     const int nstrip = (WR + SR - 1) / SR;
     float f[12], g[12];
@@ -298,7 +298,10 @@ int launch_ac(const AcArgs& a, hipStream_t s) {
   const size_t out = (size_t)TT * a.Cout * 4;
   const size_t lds = (size_t)(TT + kSpan) * PA + (raw > out ? raw : out);
   dim3 grid((a.Tmax + TT - 1) / TT, 1, a.B);
-  hipLaunchKernelGGL((amp_conv_kernel<CI, CO, TT>), grid, dim3(256), lds, s, a);
+  if (a.log_alpha)
+    hipLaunchKernelGGL((amp_conv_kernel<CI, CO, TT, true>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((amp_conv_kernel<CI, CO, TT, false>), grid, dim3(256), lds, s, a);
   return 0;
 }
 

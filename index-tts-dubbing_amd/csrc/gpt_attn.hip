@@ -38,11 +38,12 @@ __device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]
 constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is the caller's
 
 // One workgroup of NT threads per (head, sequence): NT/8 groups of 8 lanes, group g owns keys
-// g, g + NT/8, ...; lane d8 holds dims 8*d8 .. 8*d8+7.  Single pass: the K and V rows of KB keys
-// per group are loaded together (all loads of a round in flight), scores via 8-lane shuffles, an
-// online softmax per group (running max m, sum l, partial output o); groups merge through LDS.
-// (Measured on MI355X at B=32, S~283: NT = 256 beats 512-thread workgroups, and beats issuing the
-// cache loads before the q/k/v summation with 16 packed keys per group -- 308 VGPRs, 1 wave/SIMD.)
+// g, g + NT/8, ...; lane d8 holds dims 8*d8 .. 8*d8+7.  The first round's cached K and V rows (KB = 8
+// keys per group, kept packed: 256 keys at NT = 256) are requested before anything else -- they do
+// not depend on this step's q/k/v -- so their HBM latency overlaps the c_attn slab summation; later
+// rounds (S > 256) load in turn.  Scores via 8-lane shuffles, an online softmax per group (running
+// max m, sum l, partial output o); the groups merge through LDS.  (Measured alternatives, slower at
+// B=32, S~283: 512-thread workgroups; 16 packed keys per group -- 308 VGPRs, 1 wave/SIMD.)
 // q/k/v = bias + sum of `nsplit` split-K partial slabs of the c_attn GEMM (stride split_stride).
 template <typename TC, typename TO, int NT>
 __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
@@ -52,7 +53,8 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
                                                          int kv_base, const int32_t* __restrict__ tstate,
                                                          TO* __restrict__ out, int64_t ldo, int H) {
   constexpr int NG = NT / 8;
-  constexpr int KB = 8;
+  constexpr int KB = 8;                          // keys per group per round (packed rows in registers)
+  constexpr int RW = sizeof(TC) * 8 / 16;       // 16-B vectors per lane per row (bf16: 1, f32: 2)
   __shared__ float qs[kHD], kn[kHD], vn[kHD];
   __shared__ float gm[NG], gl[NG];
   __shared__ float pv[NG][kHD + 1];
@@ -60,15 +62,37 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
   const int D = H * kHD;
   const int kidx = kv_base + tstate[0];
   const int p0 = pad ? pad[b] : 0;
-  const int nk = kidx + 1 - p0;
+  const int nk = kidx + 1 - p0;  // keys p0 .. kidx; the last one is this step's (from LDS)
   TC* Kc = cache_k + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
   TC* Vc = cache_v + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
+  const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
+  // (1) the first round's cached K/V rows do not depend on this step's q/k/v: issue them first
+  u32x4_t kr[KB][RW], vr[KB][RW];
+#pragma unroll
+  for (int u = 0; u < KB; ++u) {
+    const int j = NG * u + g;
+    if (j < nk - 1) {
+#pragma unroll
+      for (int w = 0; w < RW; ++w) {
+        kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
+        vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
+      }
+    }
+  }
+  // (2) q/k/v of this step = bias + sum of the c_attn split-K slabs; new k/v appended to the cache
   if (threadIdx.x < 3 * kHD) {
     const int part = threadIdx.x / kHD, d = threadIdx.x - part * kHD;  // 0: q, 1: k, 2: v
     const int col = part * D + h * kHD + d;
     const float* src = qkv + (int64_t)b * ldqkv + col;
     float v = qkv_bias ? qkv_bias[col] : 0.f;
-    for (int s = 0; s < nsplit; ++s) v += src[s * split_stride];
+    // up to 4 slabs loaded together (independent loads in flight), summed in slab order
+    float sl[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sl[s] = s < nsplit ? src[s * split_stride] : 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (s < nsplit) v += sl[s];
+    for (int s = 4; s < nsplit; ++s) v += src[s * split_stride];
     if (part == 0) {
       qs[d] = v * 0.125f;  // 1/sqrt(64), exact
     } else if (part == 1) {
@@ -80,25 +104,35 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
     }
   }
   __syncthreads();
-  const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
   float q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) q[e] = qs[8 * d8 + e];
+  auto unpack = [&](const u32x4_t (&r)[RW], float (&x)[8]) {
+    if constexpr (sizeof(TC) == 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[2 * i] = __uint_as_float(r[0][i] << 16);
+        x[2 * i + 1] = __uint_as_float(r[0][i] & 0xFFFF0000u);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = __uint_as_float(r[i / 4][i % 4]);
+    }
+  };
+  // (3) online softmax per 8-lane group over rounds of NG*KB keys (one round for S <= 512 at bf16)
   float m = -INFINITY, l = 0.f;
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nk; j0 += NG * KB) {
-    float k[KB][8], v[KB][8];
+    if (j0 > 0) {  // later rounds (S > 512): load now
 #pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      const int j = j0 + NG * u + g;
-      if (j < nk && p0 + j != kidx) {
-        load8<TC>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8, k[u]);
-        load8<TC>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8, v[u]);
-      } else {  // the new key/value comes from LDS (never re-read the line just written)
+      for (int u = 0; u < KB; ++u) {
+        const int j = j0 + NG * u + g;
+        if (j < nk - 1) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          k[u][e] = kn[8 * d8 + e];
-          v[u][e] = vn[8 * d8 + e];
+          for (int w = 0; w < RW; ++w) {
+            kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
+            vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
+          }
         }
       }
     }
@@ -106,13 +140,21 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
     float bm = -INFINITY;
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
+      const int j = j0 + NG * u + g;
+      float kx[8];
+      if (j < nk - 1) {
+        unpack(kr[u], kx);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) kx[e] = kn[8 * d8 + e];  // this step's key (or padding)
+      }
       float part = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) part = fmaf(q[e], k[u][e], part);
+      for (int e = 0; e < 8; ++e) part = fmaf(q[e], kx[e], part);
       part += __shfl_xor(part, 1, 64);
       part += __shfl_xor(part, 2, 64);
       part += __shfl_xor(part, 4, 64);
-      s[u] = (j0 + NG * u + g < nk) ? part : -INFINITY;
+      s[u] = j < nk ? part : -INFINITY;
       bm = fmaxf(bm, s[u]);
     }
     if (bm == -INFINITY) continue;  // this group has no valid key in the round
@@ -123,10 +165,18 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
     for (int e = 0; e < 8; ++e) o[e] *= corr;
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
+      const int j = j0 + NG * u + g;
       const float pr = __expf(s[u] - mn);
       l += pr;
+      float vx[8];
+      if (j < nk - 1) {
+        unpack(vr[u], vx);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = fmaf(pr, v[u][e], o[e]);
+        for (int e = 0; e < 8; ++e) vx[e] = vn[8 * d8 + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(pr, vx[e], o[e]);
     }
     m = mn;
   }

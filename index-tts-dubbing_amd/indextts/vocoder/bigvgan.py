@@ -114,7 +114,11 @@ class _Act:
 
 
 class HipBigVGAN:
-    FUSED_CHANNELS = (24, 48)  # AMP stages run by itts_amp_conv_fwd (act fused; at C=96 separate kernels measured equal)
+    # AMP stage kernels by channel count (measured per conv on MI355X, B=32 x 400 frames):
+    #   24, 48: act fused into itts_amp_conv_fwd;  96: act kernel + itts_amp_conv_fwd without act
+    #   (the fused form ties the igemm path there, the split form beats both);  others: act + igemm
+    FUSED_CHANNELS = (24, 48)
+    SPLIT_CHANNELS = (96,)
 
     def __init__(self, state_dict, cfg_bv, device="cuda"):
         self.lib = _hip.load()
@@ -241,6 +245,7 @@ class HipBigVGAN:
             for j, layers in enumerate(self.blocks[i]):
                 src = x_st
                 fused = self.fused_amp and C in self.FUSED_CHANNELS
+                split = self.fused_amp and C in self.SPLIT_CHANNELS
                 for n, (a1, c1, a2, c2) in enumerate(layers):
                     last_layer = n == len(layers) - 1
                     alpha = (1.0 / self.nk) if (last_layer and j == self.nk - 1) else 1.0
@@ -249,6 +254,11 @@ class HipBigVGAN:
                     if fused:  # activation fused into each conv's input staging (amp_conv.hip)
                         self._amp(c1, src, t2, lens_n, a1)
                         self._amp(c2, t2, dst, lens_n, a2, r1=src, r2=r2, alpha=alpha)
+                    elif split:  # activation kernel + the all-channels conv kernel without activation
+                        self._act(a1, src, t1, lens_n)
+                        self._amp(c1, t1, t2, lens_n)
+                        self._act(a2, t2, t1, lens_n)
+                        self._amp(c2, t1, dst, lens_n, r1=src, r2=r2, alpha=alpha)
                     else:
                         self._act(a1, src, t1, lens_n)
                         self._conv(c1, t1, t2, lens_n)
