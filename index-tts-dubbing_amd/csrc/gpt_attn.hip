@@ -280,6 +280,169 @@ __global__ __launch_bounds__(kQB) void attn_prefill_kernel(const float* __restri
   }
 }
 
+// ---- MFMA flash-attention prefill (bf16 operands, f32 softmax / accumulation) -----------------
+// Used in bf16 mode (cache dtype bf16): one 256-thread workgroup = 128 queries (4 waves x 32) of one
+// head of one packed sequence.  Per 32-key tile: S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 (keys
+// are the MFMA rows, the wave's 32 queries its columns, so every lane owns one query and a row
+// softmax is 16 in-lane values + one xor-32 shuffle), online softmax, then O^T += V^T . P^T with P
+// re-packed to the B-fragment layout by one xor-32 exchange per 16 keys.  K is staged in LDS as
+// [key][dim] and V transposed as [dim][key] (bf16, padded rows), so every MFMA fragment is one
+// ds_read_b128.  Masks: causal, left padding (keys < pad) and the sequence length.  Keys of this
+// workgroup's query range are written to the decode KV cache while staging.
+constexpr int kFQ = 128;  // queries per workgroup
+constexpr int kFK = 32;   // keys per tile
+constexpr int kKP = 64 * 2 + 16;   // K tile row pitch (bytes)
+constexpr int kVP = kFK * 2 + 16;  // V^T tile row pitch (bytes)
+
+template <typename TO>
+__global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(const float* __restrict__ qkv, int64_t ldqkv,
+                                                                const int32_t* __restrict__ seq_start,
+                                                                const int32_t* __restrict__ seq_len,
+                                                                const int32_t* __restrict__ seq_pad,
+                                                                uint16_t* cache_k, uint16_t* cache_v, int64_t cache_bs,
+                                                                int64_t cache_hs, TO* __restrict__ out, int64_t ldo,
+                                                                int H) {
+  __shared__ __attribute__((aligned(16))) unsigned char Ks[kFK * kKP];
+  __shared__ __attribute__((aligned(16))) unsigned char Vt[64 * kVP];
+  const int qb = blockIdx.x, h = blockIdx.y, sq = blockIdx.z;
+  const int len = seq_len[sq], p0 = seq_pad ? seq_pad[sq] : 0;
+  const int q_lo = qb * kFQ;
+  if (q_lo >= len) return;
+  const int q_hi = min(q_lo + kFQ, len);
+  const int D = H * kHD;
+  const float* base = qkv + (int64_t)seq_start[sq] * ldqkv + h * kHD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int q = q_lo + 32 * wave + r32;  // this lane's query
+  const bool qv = q < len && q >= p0;
+  // Q^T B-fragments: lane (q, hh) holds Q[q][16ks + 8hh .. +7] * 1/8 (exact), bf16
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    float t[8];
+    if (q < len) {
+      const f32x4_t a = *reinterpret_cast<const f32x4_t*>(base + (int64_t)q * ldqkv + 16 * ks + 8 * hh);
+      const f32x4_t b = *reinterpret_cast<const f32x4_t*>(base + (int64_t)q * ldqkv + 16 * ks + 8 * hh + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { t[i] = a[i] * 0.125f; t[4 + i] = b[i] * 0.125f; }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qf[ks][i] = (__bf16)t[i];
+  }
+  f32x16_t o[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int kmax = min(q_hi, len);  // keys [p0, kmax) can be attended by this block
+  for (int k0 = (p0 / kFK) * kFK; k0 < kmax; k0 += kFK) {
+    __syncthreads();  // previous tile fully consumed
+    {  // stage K [key][dim] and V^T [dim][key] (bf16); write the cache for keys of this block's range
+      const int kk = tid >> 3, d0 = (tid & 7) * 8, key = k0 + kk;
+      float kv[8], vv[8];
+      if (key < len) {
+        const float* kr = base + (int64_t)key * ldqkv + D + d0;
+        const float* vr = base + (int64_t)key * ldqkv + 2 * D + d0;
+        const f32x4_t k0v = *reinterpret_cast<const f32x4_t*>(kr), k1v = *reinterpret_cast<const f32x4_t*>(kr + 4);
+        const f32x4_t v0v = *reinterpret_cast<const f32x4_t*>(vr), v1v = *reinterpret_cast<const f32x4_t*>(vr + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { kv[i] = k0v[i]; kv[4 + i] = k1v[i]; vv[i] = v0v[i]; vv[4 + i] = v1v[i]; }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kv[i] = vv[i] = 0.f;
+      }
+      u32x4_t kp;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) kp[i] = pack2bf(kv[2 * i], kv[2 * i + 1]);
+      *reinterpret_cast<u32x4_t*>(Ks + kk * kKP + d0 * 2) = kp;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) *reinterpret_cast<uint16_t*>(Vt + (d0 + i) * kVP + kk * 2) = f2bf(vv[i]);
+      if (cache_k && key >= q_lo && key < q_hi) {
+        uint16_t* ck = cache_k + (int64_t)sq * cache_bs + (int64_t)h * cache_hs + (int64_t)key * kHD + d0;
+        uint16_t* cv = cache_v + (int64_t)sq * cache_bs + (int64_t)h * cache_hs + (int64_t)key * kHD + d0;
+        *reinterpret_cast<u32x4_t*>(ck) = kp;
+        u32x4_t vp;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vp[i] = pack2bf(vv[2 * i], vv[2 * i + 1]);
+        *reinterpret_cast<u32x4_t*>(cv) = vp;
+      }
+    }
+    __syncthreads();
+    if (k0 > q_lo + 32 * wave + 31) continue;  // the whole tile is in this wave's causal future
+    // S^T[key][q] for keys k0 + (r&3) + 8(r>>2) + 4hh
+    f32x16_t s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(Ks + r32 * kKP + ks * 32 + hh * 16);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s, 0, 0, 0);
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (!qv || key > q || key < p0 || key >= len) s[r] = -INFINITY;
+      tmax = fmaxf(tmax, s[r]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    float psum = 0.f;
+    float pr[16];
+    if (mn == -INFINITY) {  // nothing valid yet for this query
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pr[r] = 0.f;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        pr[r] = __expf(s[r] - mn);
+        psum += pr[r];
+      }
+      const float corr = __expf(m - mn);
+      l = l * corr + psum + __shfl_xor(psum, 32, 64);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= corr;
+      m = mn;
+    }
+    // P^T B-fragments: lane (q, hh) needs P[q][keys 16ks + 8hh .. +7]; it holds keys
+    // {8j + 4hh + 0..3}: exchange one half with the xor-32 partner
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ra = 8 * ks, rb = 8 * ks + 4;  // regs of keys 16ks + 4hh + 0..3 and 16ks + 8 + 4hh + 0..3
+      const uint32_t own_lo = pack2bf(pr[ra], pr[ra + 1]), own_hi = pack2bf(pr[ra + 2], pr[ra + 3]);
+      const uint32_t own2_lo = pack2bf(pr[rb], pr[rb + 1]), own2_hi = pack2bf(pr[rb + 2], pr[rb + 3]);
+      // hh = 0 sends keys 8..11 (rb regs), hh = 1 sends keys 4..7 of the pair (ra regs)
+      const uint32_t send_lo = hh ? own_lo : own2_lo, send_hi = hh ? own_hi : own2_hi;
+      const uint32_t recv_lo = __shfl_xor(send_lo, 32, 64), recv_hi = __shfl_xor(send_hi, 32, 64);
+      u32x4_t pf;
+      if (hh == 0) {  // keys 16ks + 0..3 (own ra) then 4..7 (partner's ra)
+        pf = u32x4_t{own_lo, own_hi, recv_lo, recv_hi};
+      } else {        // keys 16ks + 8..11 (partner's rb) then 12..15 (own rb)
+        pf = u32x4_t{recv_lo, recv_hi, own2_lo, own2_hi};
+      }
+      const bf16x8_t pb = *reinterpret_cast<const bf16x8_t*>(&pf);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // O^T rows d = 32i + .. : A = V^T[d][keys 16ks + 8hh ..]
+        const bf16x8_t vf = *reinterpret_cast<const bf16x8_t*>(Vt + (32 * i + r32) * kVP + ks * 32 + hh * 16);
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, o[i], 0, 0, 0);
+      }
+    }
+  }
+  if (q >= len) return;
+  const float inv = (qv && l > 0.f) ? 1.0f / l : 0.f;
+  TO* orow = out + (int64_t)(seq_start[sq] + q) * ldo + h * kHD;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) St<TO>::st(orow + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh, o[i][r] * inv);
+}
+
 }  // namespace
 
 extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
@@ -312,8 +475,18 @@ extern "C" int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t*
   ITTS_REQUIRE(nseq >= 0 && H > 0 && max_len >= 0, fn, "bad sizes");
   if (nseq == 0 || max_len == 0) return 0;
   ITTS_REQUIRE(qkv && seq_start && seq_len && out, fn, "null pointer");
-  dim3 grid((max_len + kQB - 1) / kQB, H, nseq);
   hipStream_t s = itts::as_stream(stream);
+  if (cache_dtype == ITTS_BF16 && (ldqkv % 4) == 0 && ((reinterpret_cast<uintptr_t>(qkv) & 15) == 0)) {
+    dim3 gridf((max_len + kFQ - 1) / kFQ, H, nseq);  // product (bf16) mode: MFMA flash attention
+    if (out_dtype == ITTS_BF16)
+      hipLaunchKernelGGL((attn_prefill_mfma_kernel<uint16_t>), gridf, dim3(256), 0, s, qkv, ldqkv, seq_start, seq_len,
+                         seq_pad, (uint16_t*)cache_k, (uint16_t*)cache_v, cache_bs, cache_hs, (uint16_t*)out, ldo, H);
+    else
+      hipLaunchKernelGGL((attn_prefill_mfma_kernel<float>), gridf, dim3(256), 0, s, qkv, ldqkv, seq_start, seq_len,
+                         seq_pad, (uint16_t*)cache_k, (uint16_t*)cache_v, cache_bs, cache_hs, (float*)out, ldo, H);
+    return itts::check_launch(fn);
+  }
+  dim3 grid((max_len + kQB - 1) / kQB, H, nseq);  // verification (f32) mode: exact f32 VALU kernel
 #define ITTS_AP(TC, TO)                                                                                           \
   hipLaunchKernelGGL((attn_prefill_kernel<TC, TO>), grid, dim3(kQB), 0, s, qkv, ldqkv, seq_start, seq_len, seq_pad, \
                      (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, (TO*)out, ldo, H)

@@ -61,6 +61,33 @@ class BatchedTTS:
         self.stop = int(cfg.gpt.stop_mel_token)
         self.stop_text = int(cfg.gpt.stop_text_token)
         self._prompt_cache: Dict[object, tuple] = {}
+        self.graph_features = True  # prompt conditioning + ECAPA replayed as a captured graph
+        self._feat_graphs: Dict[tuple, tuple] = {}
+
+    @torch.no_grad()
+    def _features(self, m: torch.Tensor):
+        """conditioning latents + ECAPA speaker embedding of prompt mels m [n, 100, T]: ~300 small
+        PyTorch-ROCm launches, replayed as one captured hipGraph per (n, T) after a warm-up call."""
+        if not self.graph_features:
+            return self.gpt.conditioning(m), self.vocoder.speaker(m.transpose(1, 2))
+        key = tuple(m.shape)
+        ent = self._feat_graphs.get(key)
+        if ent is None:
+            static = m.clone()
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):  # warm-up: lets the conv libraries pick their kernels
+                self.gpt.conditioning(static), self.vocoder.speaker(static.transpose(1, 2))
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                c = self.gpt.conditioning(static)
+                s = self.vocoder.speaker(static.transpose(1, 2))
+            ent = self._feat_graphs[key] = (g, static, c, s)
+        g, static, c, s = ent
+        static.copy_(m)
+        g.replay()
+        return c.clone(), s.clone()
 
     @torch.no_grad()
     def prompt_features(self, mels: Sequence[torch.Tensor], keys: Optional[Sequence[object]] = None):
@@ -81,8 +108,7 @@ class BatchedTTS:
             by_len.setdefault(int(mels[i].shape[-1]), []).append(i)
         for idx in by_len.values():
             m = torch.cat([mels[i].reshape(1, mels[i].shape[-2], mels[i].shape[-1]) for i in idx], 0).to(self.device)
-            c = self.gpt.conditioning(m)
-            s = self.vocoder.speaker(m.transpose(1, 2))
+            c, s = self._features(m)
             for j, i in enumerate(idx):
                 feats[i] = (c[j], s[j])
                 if keys is not None:

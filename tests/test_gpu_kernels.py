@@ -147,3 +147,50 @@ def test_attn_decode_matches_torch(S, cache, nsplit):
     keep = torch.ones(smax, dtype=torch.bool)
     keep[kidx] = False
     assert torch.equal(kd[:, :, keep].cpu(), kc[:, :, keep]) and torch.equal(vd[:, :, keep].cpu(), vc[:, :, keep])
+
+
+@pytest.mark.parametrize("mode", ["bf16", "f32"])
+def test_attn_prefill_matches_torch(mode):
+    """Packed varlen causal attention with left padding (the prefill / latent-pass kernel): bf16
+    mode runs the MFMA flash kernel (bf16 Q/K/V, f32 softmax), f32 mode the exact VALU kernel.
+    vs torch fp32 on the same inputs: |err| <= 3e-2 (bf16) / 1e-4 (f32); the KV cache rows of every
+    valid position are written (bf16: rounded)."""
+    _hip, lib = _lib()
+    torch.manual_seed(7)
+    H, D = 16, 1024
+    lens = [83, 200, 1, 130, 257]
+    pads = [5, 0, 0, 17, 40]
+    starts = [0]
+    for n in lens[:-1]:
+        starts.append(starts[-1] + n)
+    M = sum(lens)
+    qkv = torch.randn(M, 3 * D)
+    smax = max(lens) + 4
+    cdt = torch.bfloat16 if mode == "bf16" else torch.float32
+    kc = torch.zeros(len(lens), H, smax, 64, dtype=cdt, device="cuda")
+    vc = torch.zeros_like(kc)
+    out = torch.zeros(M, D, dtype=cdt, device="cuda")
+    qd = qkv.cuda()
+    st_, ln_, pd_ = (torch.tensor(v, dtype=torch.int32, device="cuda") for v in (starts, lens, pads))
+    _hip.check(lib.itts_attn_prefill(qd.data_ptr(), 3 * D, st_.data_ptr(), ln_.data_ptr(), pd_.data_ptr(), len(lens),
+                                     max(lens), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
+                                     out.data_ptr(), D, H, _hip.dtype_code(kc), _hip.dtype_code(out),
+                                     _hip.stream_ptr()), "attn_prefill")
+    torch.cuda.synchronize()
+    got = out.float().cpu()
+    tol = 3e-2 if mode == "bf16" else 1e-4
+    for i, (s0, n, p) in enumerate(zip(starts, lens, pads)):
+        x = qkv[s0:s0 + n]
+        q, k, v = (x[:, j * D:(j + 1) * D].view(n, H, 64).transpose(0, 1) for j in range(3))
+        if mode == "bf16":
+            q, k, v = ((q / 8).bfloat16().float() * 8, k.bfloat16().float(), v.bfloat16().float())
+        sc = q @ k.transpose(1, 2) / 8.0
+        mask = torch.ones(n, n, dtype=torch.bool).tril()
+        mask[:, :p] = False
+        sc = sc.masked_fill(~mask, float("-inf"))
+        ref = (sc.softmax(-1).nan_to_num(0.0) @ v).transpose(0, 1).reshape(n, D)
+        g = got[s0:s0 + n]
+        assert float((g[p:] - ref[p:]).abs().max()) <= tol, (i, float((g[p:] - ref[p:]).abs().max()))
+        kk = x[:, D:2 * D].view(n, H, 64).transpose(0, 1)
+        # cache rows of every non-padding position (left-pad keys are never attended, not stored)
+        torch.testing.assert_close(kc[i, :, p:n].float().cpu(), kk[:, p:].to(cdt).float(), rtol=0, atol=0)
