@@ -14,10 +14,10 @@
 // Tile: TT (256 at C=24, 128 otherwise) output rows x all Cout columns per 256-thread workgroup
 // (4 waves, each 32-row MFMA tiles x every N tile).  LDS: raw input window (bf16, TT + taps span +
 // 12 rows), activated window (bf16, padded pitch for conflict-free ds_read_b128 MFMA fragments);
-// the raw window is reused as the f32 output tile.  Activation work item = 16 rows of one channel
-// with the up-sampled values in registers (42 snake evaluations per 16 outputs).
-// Weights: the igemm packing [tap][co_pad][ci_pad] (ci_pad, co_pad multiples of 32), fragments
-// read straight from L1/L2 with the next tap's fragments prefetched into registers.
+// a 2-slot tap-weight ring overlays the raw window, and the f32 output tile overlays everything
+// after the MFMAs.  Activation work item = 16 rows of one channel with the up-sampled values in
+// registers (42 snake evaluations per 16 outputs).  Weights: the igemm packing [tap][co_pad][ci_pad]
+// (ci_pad, co_pad multiples of 32), staged tap by tap through the LDS ring by the whole workgroup.
 #include "common.h"
 
 namespace {
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   constexpr bool act = ACT;  // compile-time: the no-activation variant keeps its registers for the conv
   const uint16_t* X = p.x + (int64_t)b * p.sxb;
   unsigned char* Aw = smem;                         // [WR][PA]
-  unsigned char* Xr = smem + (TT + kSpan) * PA;     // raw window / output tile
+  unsigned char* Xr = smem + (TT + kSpan) * PA;     // raw window, then the tap-weight ring
 
   // ---- 1. raw window -> LDS (16-B vectors); padding channels of the window zeroed ----
   const int cv8 = Cin / 8;
@@ -206,6 +206,13 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   }
 
   // ---- 3. MFMA over taps x K chunks; wave w owns output rows [32(w + 4i), +32), i < FM ----
+  // The tap weights go through a 2-slot LDS ring filled cooperatively by the whole workgroup (each
+  // weight byte crosses L2 -> CU once per block, not once per wave), next tap's loads in flight
+  // while this tap's MFMAs run; B fragments are then conflict-free ds_read_b128.
+  constexpr int PW = CIN_PAD * 2 + 16;                   // ring row pitch (bytes)
+  constexpr int WV = COUT_PAD * CIN_PAD / 8;             // 16-B vectors per tap
+  constexpr int kWV = (WV + 255) / 256;                  // per thread
+  unsigned char* Wr = Xr;                                // ring overlays the (consumed) raw window
   const int r32 = lane & 31, h = lane >> 5;
   f32x16_t acc[FM][FN];
 #pragma unroll
@@ -214,41 +221,53 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
     for (int n = 0; n < FN; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][n][r] = 0.f;
-  // weight fragments (L1/L2-resident, shared by all waves); the next tap's are prefetched into a
-  // second register set (static register names: no dynamically indexed arrays)
-  bf16x8_t wc[FN][KS], wn[FN][KS];
-  auto wload = [&](int j, bf16x8_t (&dst)[FN][KS]) {
+  u32x4_t wv[kWV];
+  auto wload = [&](int j) {
     const uint16_t* Wj = p.w + (int64_t)j * COUT_PAD * CIN_PAD;
 #pragma unroll
-    for (int n = 0; n < FN; ++n)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        dst[n][ks] = *reinterpret_cast<const bf16x8_t*>(Wj + (32 * n + r32) * CIN_PAD + ks * 16 + h * 8);
+    for (int i = 0; i < kWV; ++i) {
+      const int v = tid + 256 * i;
+      if (v < WV) wv[i] = reinterpret_cast<const u32x4_t*>(Wj)[v];
+    }
   };
-  wload(0, wc);
-  for (int j = 0; j < p.ntaps; ++j) {
-    if (j + 1 < p.ntaps) wload(j + 1, wn);
-    const int roff = r32 + p.tap_off[j] + p.hl;
+  auto wstore = [&](int slot) {
+    unsigned char* dst = Wr + slot * COUT_PAD * PW;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const unsigned char* arow = Aw + (32 * (wave + 4 * i) + roff) * PA + h * 16;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(arow + ks * 32);
-#pragma unroll
-        for (int n = 0; n < FN; ++n)
-          acc[i][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wc[n][ks], acc[i][n], 0, 0, 0);
+    for (int i = 0; i < kWV; ++i) {
+      const int v = tid + 256 * i;
+      if (v < WV) {
+        const int n = v / (CIN_PAD / 8), c = (v - n * (CIN_PAD / 8)) * 8;
+        *reinterpret_cast<u32x4_t*>(dst + n * PW + c * 2) = wv[i];
       }
     }
+  };
+  wload(0);
+  wstore(0);  // the raw window is consumed: the activation phase ended with a barrier
+  __syncthreads();
+  for (int j = 0; j < p.ntaps; ++j) {
+    if (j + 1 < p.ntaps) wload(j + 1);
+    const unsigned char* wsl = Wr + (j & 1) * COUT_PAD * PW;
+    const int roff = r32 + p.tap_off[j] + p.hl;
 #pragma unroll
-    for (int n = 0; n < FN; ++n)
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8_t bf[FN];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) wc[n][ks] = wn[n][ks];
+      for (int n = 0; n < FN; ++n) bf[n] = *reinterpret_cast<const bf16x8_t*>(wsl + (32 * n + r32) * PW + ks * 32 + h * 16);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(Aw + (32 * (wave + 4 * i) + roff) * PA + h * 16 + ks * 32);
+#pragma unroll
+        for (int n = 0; n < FN; ++n)
+          acc[i][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[n], acc[i][n], 0, 0, 0);
+      }
+    }
+    if (j + 1 < p.ntaps) wstore((j + 1) & 1);  // slot last read in tap j-1, fenced by its barrier
+    __syncthreads();
   }
-  __syncthreads();  // Xr is reused as the output tile
 
-  // ---- 4. epilogue: acc -> LDS f32 tile [TT][Cout] -> bias / residuals / alpha -> 16-B stores ----
-  float* Ys = reinterpret_cast<float*>(Xr);
+  // ---- 4. epilogue: acc -> LDS f32 tile [TT][Cout] (overlays the window + ring) -> bias /
+  //         residuals / alpha -> 16-B stores ----
+  float* Ys = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -295,8 +314,11 @@ int launch_ac(const AcArgs& a, hipStream_t s) {
   constexpr int PA = CI * 2 + 16;
   const int WR = TT + a.hl + a.hr;
   const size_t raw = a.log_alpha ? (size_t)(WR + 12) * a.Cin * 2 : 0;
-  const size_t out = (size_t)TT * a.Cout * 4;
-  const size_t lds = (size_t)(TT + kSpan) * PA + (raw > out ? raw : out);
+  const size_t ring = (size_t)2 * CO * (CI * 2 + 16);
+  const size_t win = (size_t)(TT + kSpan) * PA;
+  const size_t out = (size_t)TT * a.Cout * 4;  // overlays window + ring after the MFMAs
+  size_t lds = win + (raw > ring ? raw : ring);
+  if (lds < out) lds = out;
   dim3 grid((a.Tmax + TT - 1) / TT, 1, a.B);
   if (a.log_alpha)
     hipLaunchKernelGGL((amp_conv_kernel<CI, CO, TT, true>), grid, dim3(256), lds, s, a);

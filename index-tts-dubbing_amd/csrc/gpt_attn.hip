@@ -10,8 +10,9 @@
 //    streams 2 * S * 64 * sizeof(cache) bytes per (sequence, head).  The c_attn output may arrive
 //    as split-K partial slabs (summed here with the bias, so the GEMM needs no reduce pass).
 // 2. itts_attn_prefill: variable-length causal attention over packed sequences (prefill of the
-//    prompt block, and the teacher-forced latent pass).  One thread per query, K/V staged through
-//    LDS in 32-key blocks, block-wise online softmax; optionally writes K/V into the decode cache.
+//    prompt block, and the teacher-forced latent pass); optionally writes K/V into the decode cache.
+//    bf16 mode: MFMA flash attention (attn_prefill_mfma_kernel); f32 verification mode: one thread
+//    per query, K/V staged through LDS in 32-key blocks, exact-f32 block-wise online softmax.
 #include "common.h"
 
 namespace {
