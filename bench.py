@@ -8,13 +8,13 @@ teacher-forced latent pass, BigVGAN2 -> int16 PCM; with N>1 ranks the finished w
 to rank 0 over RCCL (utterances shard data-parallel, weak scaling).  Inputs are resident in HBM when
 the timed region starts; weights are seeded random-init IndexTTS-1.5 (no checkpoints are available).
 
-Also reports ``roofline``: the MFMA implicit-GEMM that runs every BigVGAN conv (the largest
-eagerly-launched kernel family), achieved TFLOP/s from HIP events around each launch over the timed
-region, its algorithmic bytes per launch and, when profiles/traffic_r01.json exists, the HBM bytes per
-launch from the rocprofv3 PMC passes (profiles/pmc_vocoder.py); ``roofline_gpt_decode``: the
-hipGraph-replayed GPT decode step (weights + KV cache bytes per step / step time, HIP events around
-each replay); and a CPU baseline: the fp32 oracle (a CPU restatement of the reference path) on a
-bounded sample, on this host's cores.
+Also reports ``roofline``: the dominant unit of work, the hipGraph-replayed GPT decode step (>60 % of
+the step; HBM-bound): algorithmic bytes (every weight byte + the K/V rows attended) per replay /
+the replay's duration from HIP events recorded on the decode stream around each replay, and
+``traffic`` = measured HBM bytes per step from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+(profiles/run_profiles.sh -> profiles/traffic_decode_r01.json); ``roofline_vocoder_conv``: the MFMA
+implicit GEMM running the BigVGAN convs (HIP events around each launch); and ``cpu_baseline``: the
+fp32 oracle (a CPU restatement of the reference path) on a bounded sample, on this host's cores.
 """
 import argparse
 import json
@@ -78,6 +78,16 @@ def install_conv_timer(voc, timer):
         return timer.wrap(lambda: orig(c, x, y, lens, **kw), 2.0 * rows * c.cout * c.cin * c.ntaps, nbytes)
 
     voc._conv = timed
+
+
+def _traffic(name, key):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/run_profiles.sh)."""
+    path = os.path.join(REPO, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        v = json.load(f).get(key)
+    return None if v is None else round(float(v))
 
 
 def make_inputs(cfg, indices, L, frames):
@@ -209,16 +219,15 @@ def main():
         dist.destroy_process_group()
         return
     achieved = (k_flops / (k_ms * 1e-3) / 1e12) if k_ms > 0 else None
-    roof = {"kernel": "itts_igemm_fwd (BigVGAN convs, MFMA bf16)", "bound": "mfma",
-            "achieved": None if achieved is None else round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
-            "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / PEAK_BF16_TFLOPS, 4),
-            "traffic": None, "launches": k_n, "avg_launch_us": round(1e3 * k_ms / max(k_n, 1), 2),
-            "algorithmic_bytes_per_launch": round(timer.bytes / max(k_n, 1)),
-            "share_of_step": round(k_ms / (1e3 * dt), 3)}
-    tf = os.path.join(REPO, "profiles", "traffic_r01.json")
-    if os.path.exists(tf):
-        with open(tf) as f:
-            roof["traffic"] = json.load(f).get("igemm_bytes_per_launch")
+    voc = {"kernel": "itts_igemm_fwd (BigVGAN convs C >= 192 and ConvTranspose phases, MFMA bf16)", "bound": "mfma",
+           "achieved": None if achieved is None else round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
+           "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / PEAK_BF16_TFLOPS, 4),
+           "traffic": _traffic("traffic_vocoder_r01.json", "igemm_bytes_per_launch"), "launches": k_n,
+           "avg_launch_us": round(1e3 * k_ms / max(k_n, 1), 2),
+           "algorithmic_bytes_per_launch": round(timer.bytes / max(k_n, 1)),
+           "share_of_step": round(k_ms / (1e3 * dt), 3)}
+    if dec is not None:  # the decode step is the dominant unit of work (>60 % of the step)
+        dec["traffic"] = _traffic("traffic_decode_r01.json", "bytes_per_step")
     cpu = None
     if args.breakdown:
         ph = {}
@@ -235,8 +244,8 @@ def main():
                                f"{N} codes each (EOS suppressed): conditioning+ECAPA, GPT prefill+decode (hipGraph), "
                                "latent pass, BigVGAN2 -> int16", "global_batch": B * world, "seq_len": N,
                    "parallelism": f"dp{world}"},
-        "roofline": roof,
-        "roofline_gpt_decode": dec,
+        "roofline": dec,
+        "roofline_vocoder_conv": voc,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Profiling pass on the GPU box (run from the repo root via gpurun):
+#   1. rocprofv3 --kernel-trace --stats of bench.py (C3)  -> gpurun_out/kernel_stats.csv
+#   2. FETCH_SIZE / WRITE_SIZE passes (one counter group per run) over the GPT decode step and the
+#      vocoder                                            -> gpurun_out/traffic_{decode,vocoder}.json
+# Large traces stay under /tmp on the box; only the small summaries come back.
+set -e
+export TMPDIR=/tmp
+TAG=${1:-r01}
+mkdir -p gpurun_out
+rm -rf /tmp/prof /tmp/pmc_*
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof -o run -- \
+    python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof_$TAG.log 2>&1
+cp "$(find /tmp/prof -name '*kernel_stats.csv' | head -n 1)" gpurun_out/kernel_stats_$TAG.csv
+python3 profiles/summarize.py gpurun_out/kernel_stats_$TAG.csv 2 > gpurun_out/kernel_stats_$TAG.txt
+if [ "${2:-pmc}" = "pmc" ]; then
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pmc_df -o run -- python3 profiles/pmc_decode.py > gpurun_out/pmc_df.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pmc_dw -o run -- python3 profiles/pmc_decode.py > gpurun_out/pmc_dw.log 2>&1
+  python3 profiles/traffic.py decode /tmp/pmc_df /tmp/pmc_dw > gpurun_out/traffic_decode_$TAG.json
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pmc_vf -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vf.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pmc_vw -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vw.log 2>&1
+  python3 profiles/traffic.py vocoder /tmp/pmc_vf /tmp/pmc_vw > gpurun_out/traffic_vocoder_$TAG.json
+fi
+echo profiles-done

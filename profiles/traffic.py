@@ -1,12 +1,16 @@
-"""Per-launch HBM traffic of the vocoder conv kernel from two rocprofv3 PMC passes.
+"""Per-launch HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE in separate runs).
 
-FETCH_SIZE and WRITE_SIZE (KiB per dispatch) come from separate passes (they do not fit in one
-TCC pass on gfx950).  Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section), gfx950 FETCH_SIZE
-reports half the bytes of wide coalesced streaming reads, so it is doubled; WRITE_SIZE is exact for
-16-B-per-lane stores.  Only the second half of the ``igemm_kernel`` dispatches (the second forward
-of profiles/pmc_vocoder.py) is averaged.
+FETCH_SIZE and WRITE_SIZE (KiB per dispatch) do not fit in one TCC pass on gfx950.  Per
+/opt/skills/guides/MI355X_MICROARCH.md (HBM section), gfx950 FETCH_SIZE reports half the bytes of
+wide coalesced streaming reads, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
 
-usage: python profiles/traffic.py <fetch_dir> <write_dir>  -> JSON on stdout
+usage:
+  python profiles/traffic.py vocoder <fetch_dir> <write_dir>
+      igemm_kernel dispatches of the second of two vocoder forwards (profiles/pmc_vocoder.py)
+  python profiles/traffic.py decode <fetch_dir> <write_dir>
+      the GPT decode-step kernels (profiles/pmc_decode.py), summed per step; one step = one
+      advance_kernel dispatch; dispatches before the first attn_decode_kernel (prefill) skipped
+-> JSON on stdout
 """
 import csv
 import glob
@@ -14,35 +18,69 @@ import json
 import os
 import sys
 
+DECODE_KERNELS = ("attn_decode_kernel", "decode_gemm_kernel", "residual_reduce_ln", "sample_embed_kernel",
+                  "sample_topk_embed_kernel", "advance_kernel")
 
-def per_dispatch(d, counter):
+
+def load(d, counter):
+    """-> {dispatch_id: (kernel_name, value)}"""
     path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     vals = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "igemm_kernel" not in r["Kernel_Name"]:
+        if r["Counter_Name"] != counter:
             continue
         k = int(r["Dispatch_Id"])
-        vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
-    ids = sorted(vals)
-    ids = ids[len(ids) // 2:]
-    return [vals[i] for i in ids]
+        name, v = vals.get(k, (r["Kernel_Name"], 0.0))
+        vals[k] = (name, v + float(r["Counter_Value"]))
+    return vals
+
+
+def short(name):
+    for k in DECODE_KERNELS + ("igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel"):
+        if k in name:
+            return k
+    return name.split("(")[0][-40:]
+
+
+def vocoder(fetch, write):
+    out = {"kernel": "igemm_kernel (BigVGAN convs, second of two C3 vocoder forwards)"}
+    for name in ("igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel"):
+        ids = sorted(k for k, (n, _) in fetch.items() if name in n and k in write)
+        ids = ids[len(ids) // 2:]
+        if not ids:
+            continue
+        fb = sum(2 * 1024 * fetch[i][1] for i in ids) / len(ids)  # KiB -> bytes, x2 gfx950 correction
+        wb = sum(1024 * write[i][1] for i in ids) / len(ids)
+        out[name] = {"dispatches": len(ids), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                     "bytes_per_launch": fb + wb}
+    out["igemm_bytes_per_launch"] = out.get("igemm_kernel", {}).get("bytes_per_launch")
+    out["correction"] = "FETCH_SIZE x2 (gfx950 coalesced-read undercount); KiB -> bytes"
+    return out
+
+
+def decode(fetch, write):
+    ids = sorted(k for k, (n, _) in fetch.items() if k in write)
+    first = min(k for k in ids if "attn_decode_kernel" in fetch[k][0])
+    ids = [k for k in ids if k >= first and any(s in fetch[k][0] for s in DECODE_KERNELS)]
+    steps = sum(1 for k in ids if "advance_kernel" in fetch[k][0])
+    per = {}
+    for k in ids:
+        n = short(fetch[k][0])
+        f, w, c = per.get(n, (0.0, 0.0, 0))
+        per[n] = (f + 2 * 1024 * fetch[k][1], w + 1024 * write[k][1], c + 1)
+    tot_f = sum(v[0] for v in per.values()) / steps
+    tot_w = sum(v[1] for v in per.values()) / steps
+    return {"kernel": "GPT decode step (all decode-step dispatches, graph disabled)", "steps": steps,
+            "fetch_bytes_per_step": tot_f, "write_bytes_per_step": tot_w, "bytes_per_step": tot_f + tot_w,
+            "per_kernel_per_step": {n: {"launches": c // steps, "fetch_bytes": f / steps, "write_bytes": w / steps}
+                                    for n, (f, w, c) in per.items()},
+            "correction": "FETCH_SIZE x2 (gfx950 coalesced-read undercount); KiB -> bytes"}
 
 
 def main():
-    fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
-    write = per_dispatch(sys.argv[2], "WRITE_SIZE")
-    n = min(len(fetch), len(write))
-    fetch_b = [2 * 1024 * v for v in fetch[:n]]  # KiB -> bytes, x2 gfx950 correction
-    write_b = [1024 * v for v in write[:n]]
-    out = {
-        "kernel": "igemm_kernel (BigVGAN convs, second of two C3 vocoder forwards)",
-        "dispatches": n,
-        "fetch_bytes_per_launch": sum(fetch_b) / n,
-        "write_bytes_per_launch": sum(write_b) / n,
-        "igemm_bytes_per_launch": (sum(fetch_b) + sum(write_b)) / n,
-        "correction": "FETCH_SIZE x2 (gfx950 coalesced-read undercount); KiB -> bytes",
-    }
-    print(json.dumps(out, indent=1))
+    mode, fdir, wdir = sys.argv[1:4]
+    fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    print(json.dumps(vocoder(fetch, write) if mode == "vocoder" else decode(fetch, write), indent=1))
 
 
 if __name__ == "__main__":
