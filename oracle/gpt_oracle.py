@@ -148,6 +148,152 @@ class GPTOracle:
         codes = torch.stack(out, 1)
         return (codes, trace) if return_trace else codes
 
+    # ---------------- beam search / beam sample (HF 4.36 semantics) ----------------
+    @staticmethod
+    def warp(sc: torch.Tensor, temperature: float, top_k: int, top_p: float, min_keep: int):
+        """Temperature -> TopK -> TopP warpers (HF:generation/logits_process.py TemperatureLogitsWarper,
+        TopKLogitsWarper, TopPLogitsWarper), row-wise; min_keep = 2 under beams (HF 4.36
+        ``_get_logits_warper``: eos is a single id)."""
+        if temperature != 1.0:
+            sc = sc / temperature
+        if top_k:
+            k = min(max(top_k, min_keep), sc.shape[-1])
+            kth = torch.topk(sc, k, dim=-1).values[..., -1:]
+            sc = sc.masked_fill(sc < kth, float("-inf"))
+        if top_p < 1.0:
+            srt, idx = torch.sort(sc, descending=False, dim=-1)
+            cum = srt.softmax(-1).cumsum(-1)
+            rem = cum <= (1 - top_p)
+            rem[..., -min_keep:] = False
+            sc = sc.masked_fill(rem.scatter(-1, idx, rem), float("-inf"))
+        return sc
+
+    def generate_beam(self, conds, text_ids, max_new_tokens: int, num_beams: int = 3,
+                      repetition_penalty: float = 10.0, length_penalty: float = 0.0, min_new_tokens: int = 0,
+                      do_sample: bool = False, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
+                      generator: Optional[torch.Generator] = None):
+        """``generate(num_beams=K)`` as transformers 4.36 runs it for ``inference_speech``
+        (gpt/model.py:698-703): ``beam_search`` (do_sample=False) or ``beam_sample`` (do_sample=True)
+        with ``BeamSearchScorer`` (HF:generation/beam_search.py process / finalize, BeamHypotheses
+        add / is_done; early_stopping=False, one returned sequence per input).
+
+        * step scores = log_softmax(logits) -> repetition penalty over each beam's whole sequence
+          (fake prefix included, Q4; on log-probs, so x*penalty) -> min_new_tokens mask;
+          beam_sample then applies the warpers (min_keep 2) before the running beam score is added;
+        * beam_search starts beams 1..K-1 at -1e9 (only beam 0 expands at the first step),
+          beam_sample starts every beam at 0 (identical first-step rows: duplicate beams possible);
+        * 2K candidates per utterance over the [K x V] scores: top-k (search) or multinomial without
+          replacement from softmax(scores) sorted by score (sample); an eos candidate ranked < K closes a
+          hypothesis (score / generated_len ** length_penalty, generated_len counting the eos slot),
+          the first K non-eos candidates become the new beams;
+        * an utterance is done once it holds K hypotheses and its worst one >= best candidate score /
+          generated_len ** length_penalty; at max length the open beams are added as hypotheses.
+        -> codes [B, n]: the best hypothesis per utterance, then the stop token (eos), padded with it.
+        """
+        emb, mask = self.prepare_inputs(conds, text_ids)
+        B, s, D = emb.shape
+        K = int(num_beams)
+        sd = self.sd
+        V = sd["mel_head.weight"].shape[0]
+        stop = self.stop_mel
+        start = sd["mel_embedding.weight"][self.start_mel] + sd["mel_pos_embedding.emb.weight"][0]
+        x = torch.cat([emb, start.expand(B, 1, D)], 1)
+        kv: List[Optional[tuple]] = [None] * self.L
+        h = self.core(x, self._bias(mask, s + 1), kv)
+        rows = torch.arange(B).repeat_interleave(K)  # row b*K + k <- utterance b
+        kv = [(k[rows], v[rows]) for k, v in kv]
+        mask = mask[rows]
+        logits = self.head(h[:, -1])[rows]
+        R = B * K
+        seen = torch.zeros(R, V, dtype=torch.bool)
+        seen[:, 1] = True
+        seen[:, self.start_mel] = True
+        seqs = [[] for _ in range(R)]
+        beam_scores = torch.zeros(B, K)
+        if not do_sample:
+            beam_scores[:, 1:] = -1e9
+        hyps = [[] for _ in range(B)]  # list order matters for ties: (score, tokens)
+        worst = [1e9] * B
+        done = [False] * B
+
+        def add(b, toks, score, glen):
+            sc_ = score / (glen ** length_penalty)
+            if len(hyps[b]) < K or sc_ > worst[b]:
+                hyps[b].append((sc_, list(toks)))
+                if len(hyps[b]) > K:
+                    order = sorted((hs, i) for i, (hs, _) in enumerate(hyps[b]))
+                    del hyps[b][order[0][1]]
+                    worst[b] = order[1][0]
+                else:
+                    worst[b] = min(sc_, worst[b])
+
+        for step in range(max_new_tokens):
+            lp = torch.log_softmax(logits, -1)
+            sc = self.penalize(lp, seen, repetition_penalty)
+            if step < min_new_tokens:
+                sc[:, stop] = float("-inf")
+            if do_sample:
+                sc = self.warp(sc, temperature, top_k, top_p, 2)
+            sc = (sc + beam_scores.reshape(R, 1)).reshape(B, K * V)
+            if do_sample:
+                idx = torch.multinomial(torch.softmax(sc, -1), 2 * K, generator=generator)
+                vals = torch.gather(sc, 1, idx)
+                vals, order = torch.sort(vals, descending=True, dim=1)
+                idx = torch.gather(idx, 1, order)
+            else:
+                vals, idx = torch.topk(sc, 2 * K, dim=1)
+            glen = step + 1
+            parent = torch.zeros(R, dtype=torch.long)
+            token = torch.full((R,), stop, dtype=torch.long)
+            new_scores = torch.zeros(B, K)
+            for b in range(B):
+                if done[b]:
+                    parent[b * K:(b + 1) * K] = torch.arange(b * K, (b + 1) * K)
+                    continue
+                j = 0
+                for rank in range(2 * K):
+                    t, p, v = int(idx[b, rank] % V), int(idx[b, rank] // V), float(vals[b, rank])
+                    if t == stop:
+                        if rank >= K:
+                            continue
+                        add(b, seqs[b * K + p], v, glen)
+                    else:
+                        new_scores[b, j], token[b * K + j], parent[b * K + j] = v, t, b * K + p
+                        j += 1
+                    if j == K:
+                        break
+                if len(hyps[b]) >= K and worst[b] >= float(vals[b].max()) / (glen ** length_penalty):
+                    done[b] = True
+            if all(done):
+                break
+            # reorder the beams (HF _reorder_cache / input_ids[beam_idx]) and append the new tokens
+            kv = [(k[parent], v[parent]) for k, v in kv]
+            seen = seen[parent]
+            seqs = [seqs[int(parent[r])] + [int(token[r])] for r in range(R)]
+            seen[torch.arange(R), token] = True
+            beam_scores = new_scores
+            if step == max_new_tokens - 1:
+                break
+            mask = torch.cat([mask, torch.ones(R, 1, dtype=mask.dtype)], 1)
+            pos = mask.shape[1] - s  # quirk Q1
+            e = sd["mel_embedding.weight"][token] + sd["mel_pos_embedding.emb.weight"][pos]
+            h = self.core(e[:, None], self._bias(mask, 1), kv)
+            logits = self.head(h[:, -1])
+        for b in range(B):  # finalize
+            if done[b]:
+                continue
+            for k in range(K):
+                add(b, seqs[b * K + k], float(beam_scores[b, k]), len(seqs[b * K + k]))
+        best = []
+        for b in range(B):
+            srt = sorted(hyps[b], key=lambda t: t[0])
+            best.append(srt[-1][1])
+        n = min(max(len(t) for t in best) + 1, max_new_tokens)
+        out = torch.full((B, n), stop, dtype=torch.long)
+        for b, t in enumerate(best):
+            out[b, :len(t)] = torch.tensor(t, dtype=torch.long)
+        return out
+
     def forced_logits(self, conds, text_ids, codes: torch.Tensor):
         """Teacher-forced decode: the logits (after penalty) the generate loop sees at each step when
         fed ``codes`` -> [B, n, V]. Lets fixtures compare per-step logits without free-running drift."""

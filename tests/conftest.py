@@ -27,3 +27,9 @@ def pytest_collection_modifyitems(config, items):
 def golden():
     import numpy as np
     return np.load(os.path.join(REPO, "tests", "golden", "golden.npz"))
+
+
+@pytest.fixture(scope="session")
+def beam_golden():
+    import numpy as np
+    return np.load(os.path.join(REPO, "tests", "golden", "beam_golden.npz"))
