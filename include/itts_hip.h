@@ -113,6 +113,14 @@ int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_
                      void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs, int smax, const int32_t* pad,
                      int kv_base, const int32_t* tstate, void* out, int64_t ldo, int B, int H, int cache_dtype,
                      int out_dtype, void* stream);
+/* Beam variant (num_beams > 1): key position p of row b is read from cache row kv_rows[b*ld_rows + p]
+ * (the beams' shared-prefix lineage; replaces HF's per-step _reorder_cache index_select of every
+ * layer's K/V, gpt/model.py:194-207); this step's k/v are appended to row b. */
+int itts_attn_decode_rows(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride, const float* qkv_bias,
+                          void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs, int smax,
+                          const int32_t* pad, int kv_base, const int32_t* tstate, void* out, int64_t ldo, int B,
+                          int H, int cache_dtype, int out_dtype, const int32_t* kv_rows, int64_t ld_rows,
+                          void* stream);
 /* Causal attention over packed variable-length sequences (prefill and latent pass); optionally
  * writes K/V into the decode cache.  seq_pad[b] leading rows are masked (left padding, Q2). */
 int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start, const int32_t* seq_len,
@@ -139,6 +147,31 @@ int itts_sample_topk_embed(const float* logits, int64_t ldl, int V, uint8_t* see
                            float temperature, int top_k, float top_p, const float* emb, const float* pos_emb,
                            int pos_delta, int D, const float* ln_g, const float* ln_b, float* x, void* h,
                            int h_dtype, int B, const int32_t* forced, void* stream);
+/* Beam search / beam sample step, part 1 (rows R = utterances x num_beams, 2 <= num_beams <= 8):
+ * per row log_softmax -> repetition penalty on the log-probs (Q4) -> min_new_tokens -> [do_sample:
+ * Temperature -> TopK -> TopP, min_keep 2] -> + running beam score; writes the row's 2*num_beams best
+ * (key, score, token) candidates (key = score, or score + Gumbel noise when sampling: a without-
+ * replacement multinomial draw).  HF 4.36 beam_search / beam_sample (generation/utils.py), called by
+ * inference_speech's generate (gpt/model.py:698-703) with infer.py:535-543's defaults. */
+int itts_beam_candidates(const float* logits, int64_t ldl, int V, const uint8_t* seen, float* beam_score,
+                         const int32_t* tstate, int col_delta, int min_new, int stop, float penalty, int do_sample,
+                         float temperature, int top_k, float top_p, int num_beams, float* cand_key,
+                         float* cand_score, int32_t* cand_tok, int R, void* stream);
+/* Part 2, per utterance: top 2K of its K x 2K candidates (sampling: sorted by score), then
+ * BeamSearchScorer.process (HF generation/beam_search.py: eos ranked < K closes a hypothesis scored
+ * sum_logprobs / generated_len**length_penalty; the first K non-eos candidates continue; done once K
+ * hypotheses exist and the worst >= the best candidate), beam reorder of the running codes, the
+ * repetition-penalty flags and the KV lineage table, next input embedding + ln_1 (as
+ * itts_sample_embed).  Hypotheses live in hyp_* ([B][K] scores/lengths/list order, [B][K][ldc] codes);
+ * the caller finalizes (adds the open beams of unfinished utterances, picks the best). */
+int itts_beam_select(const float* cand_key, const float* cand_score, const int32_t* cand_tok, int num_beams, int V,
+                     int stop, int do_sample, float length_penalty, const int32_t* tstate, int col_delta,
+                     uint8_t* done, float* beam_score, int32_t* codes, int64_t ldc, uint8_t* seen, int64_t lds,
+                     const int32_t* base_ids, int n_base, int32_t* kv_rows, int64_t ld_rows, int kv_base,
+                     float* hyp_score, int32_t* hyp_len, int32_t* hyp_codes, int32_t* hyp_n, int32_t* hyp_order,
+                     float* hyp_worst, const float* emb, const float* pos_emb, int pos_delta, int D,
+                     const float* ln_g, const float* ln_b, float* x, void* h, int h_dtype, int B, int max_col,
+                     void* stream);
 /* tstate[0] += delta on the device (advances the decode column between graph replays). */
 int itts_step_advance(int32_t* tstate, int delta, void* stream);
 

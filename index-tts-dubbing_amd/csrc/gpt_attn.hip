@@ -46,13 +46,17 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 // max m, sum l, partial output o); the groups merge through LDS.  (Measured alternatives, slower at
 // B=32, S~283: 512-thread workgroups; 16 packed keys per group -- 308 VGPRs, 1 wave/SIMD.)
 // q/k/v = bias + sum of `nsplit` split-K partial slabs of the c_attn GEMM (stride split_stride).
-template <typename TC, typename TO, int NT>
+// ROWS (beam search): key position p of sequence b lives in cache row kv_rows[b * ld_rows + p] (beams
+// share their common prefix, HF's per-step cache reorder becomes this lineage table); this step's
+// key/value go to the sequence's own row b.
+template <typename TC, typename TO, int NT, bool ROWS>
 __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
                                                          int64_t split_stride, const float* __restrict__ qkv_bias,
                                                          TC* __restrict__ cache_k, TC* __restrict__ cache_v,
                                                          int64_t cache_bs, int64_t cache_hs, const int32_t* pad,
                                                          int kv_base, const int32_t* __restrict__ tstate,
-                                                         TO* __restrict__ out, int64_t ldo, int H) {
+                                                         TO* __restrict__ out, int64_t ldo, int H,
+                                                         const int32_t* __restrict__ kv_rows, int64_t ld_rows) {
   constexpr int NG = NT / 8;
   constexpr int KB = 8;                          // keys per group per round (packed rows in registers)
   constexpr int RW = sizeof(TC) * 8 / 16;       // 16-B vectors per lane per row (bf16: 1, f32: 2)
@@ -66,6 +70,12 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
   const int nk = kidx + 1 - p0;  // keys p0 .. kidx; the last one is this step's (from LDS)
   TC* Kc = cache_k + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
   TC* Vc = cache_v + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
+  const int32_t* rows = ROWS ? kv_rows + (int64_t)b * ld_rows : nullptr;
+  // element offset of key position p (relative to Kc / Vc)
+  auto koff = [&](int p) -> int64_t {
+    if constexpr (ROWS) return (int64_t)(rows[p] - b) * cache_bs + (int64_t)p * kHD;
+    else return (int64_t)p * kHD;
+  };
   const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
   // (1) the first round's cached K/V rows do not depend on this step's q/k/v: issue them first
   u32x4_t kr[KB][RW], vr[KB][RW];
@@ -75,8 +85,8 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
     if (j < nk - 1) {
 #pragma unroll
       for (int w = 0; w < RW; ++w) {
-        kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
-        vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
+        kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + koff(p0 + j) + 8 * d8)[w];
+        vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + koff(p0 + j) + 8 * d8)[w];
       }
     }
   }
@@ -131,8 +141,8 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
         if (j < nk - 1) {
 #pragma unroll
           for (int w = 0; w < RW; ++w) {
-            kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
-            vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + (int64_t)(p0 + j) * kHD + 8 * d8)[w];
+            kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + koff(p0 + j) + 8 * d8)[w];
+            vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + koff(p0 + j) + 8 * d8)[w];
           }
         }
       }
@@ -446,11 +456,12 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(const float* __r
 
 }  // namespace
 
-extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
-                                const float* qkv_bias, void* cache_k, void* cache_v, int64_t cache_bs,
-                                int64_t cache_hs, int smax, const int32_t* pad, int kv_base, const int32_t* tstate,
-                                void* out, int64_t ldo, int B, int H, int cache_dtype, int out_dtype, void* stream) {
-  const char* fn = "itts_attn_decode";
+namespace {
+int attn_decode_launch(const char* fn, const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
+                       const float* qkv_bias, void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs,
+                       int smax, const int32_t* pad, int kv_base, const int32_t* tstate, void* out, int64_t ldo,
+                       int B, int H, int cache_dtype, int out_dtype, const int32_t* kv_rows, int64_t ld_rows,
+                       void* stream) {
   ITTS_REQUIRE(B >= 0 && H > 0 && nsplit >= 1, fn, "bad sizes");
   if (B == 0) return 0;
   ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && out, fn, "null pointer");
@@ -458,14 +469,44 @@ extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int
   dim3 grid(H, B);
   hipStream_t s = itts::as_stream(stream);
 #define ITTS_AD(TC, TO)                                                                                             \
-  hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit, split_stride,    \
-                     qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base, tstate, (TO*)out, ldo, H)
+  do {                                                                                                            \
+    if (kv_rows)                                                                                                  \
+      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, true>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,       \
+                         split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base,      \
+                         tstate, (TO*)out, ldo, H, kv_rows, ld_rows);                                               \
+    else                                                                                                          \
+      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, false>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,      \
+                         split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base,      \
+                         tstate, (TO*)out, ldo, H, nullptr, 0);                                                     \
+  } while (0)
   if (cache_dtype == ITTS_BF16 && out_dtype == ITTS_BF16) ITTS_AD(uint16_t, uint16_t);
   else if (cache_dtype == ITTS_F32 && out_dtype == ITTS_F32) ITTS_AD(float, float);
   else if (cache_dtype == ITTS_BF16) ITTS_AD(uint16_t, float);
   else ITTS_AD(float, uint16_t);
 #undef ITTS_AD
   return itts::check_launch(fn);
+}
+}  // namespace
+
+extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
+                                const float* qkv_bias, void* cache_k, void* cache_v, int64_t cache_bs,
+                                int64_t cache_hs, int smax, const int32_t* pad, int kv_base, const int32_t* tstate,
+                                void* out, int64_t ldo, int B, int H, int cache_dtype, int out_dtype, void* stream) {
+  return attn_decode_launch("itts_attn_decode", qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v,
+                            cache_bs, cache_hs, smax, pad, kv_base, tstate, out, ldo, B, H, cache_dtype, out_dtype,
+                            nullptr, 0, stream);
+}
+
+extern "C" int itts_attn_decode_rows(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
+                                     const float* qkv_bias, void* cache_k, void* cache_v, int64_t cache_bs,
+                                     int64_t cache_hs, int smax, const int32_t* pad, int kv_base,
+                                     const int32_t* tstate, void* out, int64_t ldo, int B, int H, int cache_dtype,
+                                     int out_dtype, const int32_t* kv_rows, int64_t ld_rows, void* stream) {
+  const char* fn = "itts_attn_decode_rows";
+  ITTS_REQUIRE(kv_rows && ld_rows >= smax, fn, "kv_rows [B][ld_rows >= smax] required");
+  return attn_decode_launch(fn, qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v, cache_bs, cache_hs,
+                            smax, pad, kv_base, tstate, out, ldo, B, H, cache_dtype, out_dtype, kv_rows, ld_rows,
+                            stream);
 }
 
 extern "C" int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start, const int32_t* seq_len,

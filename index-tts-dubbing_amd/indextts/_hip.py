@@ -48,6 +48,13 @@ SIGNATURES = {
     "itts_attn_decode": (_c_i, [_vp, _c_i64, _c_i, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _c_i, _vp, _c_i, _vp, _vp,
                                 _c_i64, _c_i, _c_i,
                                 _c_i, _c_i, _vp]),
+    "itts_attn_decode_rows": (_c_i, [_vp, _c_i64, _c_i, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _c_i, _vp, _c_i, _vp,
+                                     _vp, _c_i64, _c_i, _c_i, _c_i, _c_i, _vp, _c_i64, _vp]),
+    "itts_beam_candidates": (_c_i, [_vp, _c_i64, _c_i, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_f, _c_i, _c_f, _c_i, _c_f,
+                                    _c_i, _vp, _vp, _vp, _c_i, _vp]),
+    "itts_beam_select": (_c_i, [_vp, _vp, _vp, _c_i, _c_i, _c_i, _c_i, _c_f, _vp, _c_i, _vp, _vp, _vp, _c_i64, _vp,
+                                _c_i64, _vp, _c_i, _vp, _c_i64, _c_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i,
+                                _c_i, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _vp]),
     "itts_attn_prefill": (_c_i, [_vp, _c_i64, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i,
                                  _c_i, _c_i, _vp]),
     "itts_sample_embed": (_c_i, [_vp, _c_i64, _c_i, _vp, _vp, _vp, _c_i64, _vp, _c_i, _c_i, _c_i, _c_f, _vp, _vp, _c_i,

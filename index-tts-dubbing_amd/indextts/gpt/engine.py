@@ -245,10 +245,17 @@ class HipGPT:
                 kq, qkv_bias = self._ksplit(ly.w["qkv"]["K"], self.KSPLIT["qkv"]), ly.b["qkv"]
                 self._dg(h, ly.w["qkv"], B, None, qkv, epi=2, ksplit=kq)
             kc, vc = st["kc"][li], st["vc"][li]
-            _hip.check(self.lib.itts_attn_decode(
-                qkv.data_ptr(), 3 * D, kq, B * 3 * D, _hip.ptr(qkv_bias), kc.data_ptr(), vc.data_ptr(), kc.stride(0),
-                kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(), o.data_ptr(), D, B,
-                self.H, _hip.dtype_code(kc), _hip.dtype_code(o), stream), "itts_attn_decode")
+            if "kv_rows" in st:  # beams: keys read through the lineage table
+                _hip.check(self.lib.itts_attn_decode_rows(
+                    qkv.data_ptr(), 3 * D, kq, B * 3 * D, _hip.ptr(qkv_bias), kc.data_ptr(), vc.data_ptr(),
+                    kc.stride(0), kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(),
+                    o.data_ptr(), D, B, self.H, _hip.dtype_code(kc), _hip.dtype_code(o), st["kv_rows"].data_ptr(),
+                    st["kv_rows"].stride(0), stream), "itts_attn_decode_rows")
+            else:
+                _hip.check(self.lib.itts_attn_decode(
+                    qkv.data_ptr(), 3 * D, kq, B * 3 * D, _hip.ptr(qkv_bias), kc.data_ptr(), vc.data_ptr(),
+                    kc.stride(0), kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(),
+                    o.data_ptr(), D, B, self.H, _hip.dtype_code(kc), _hip.dtype_code(o), stream), "itts_attn_decode")
             nxt = self.layers[li + 1].ln1 if li + 1 < self.L else None
             if self.mode == "f32":
                 self._gemm(o[:B], ly.w["o"], x, bias=ly.b["o"], residual=True)
@@ -274,7 +281,10 @@ class HipGPT:
             self._gemm(h[:B], self.head_w, st["logits"], bias=self.head_b)
         else:
             self._dg(h, self.head_w, B, self.head_b, st["logits"])
-        self._sample(st, 1, min_new, penalty)
+        if "kv_rows" in st:
+            self._beam_step(st, 1)
+        else:
+            self._sample(st, 1, min_new, penalty)
         _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
     # split-K factors of the residual projections (partials reduced by itts_residual_reduce_ln)
@@ -345,11 +355,18 @@ class HipGPT:
                  repetition_penalty: float = 10.0, min_new_tokens: int = 0, use_graph: bool = True,
                  check_every: int = 16, forced_codes: Optional[torch.Tensor] = None, do_sample: bool = False,
                  temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
-                 seed: Optional[int] = None, lanes: Optional[int] = None) -> torch.Tensor:
+                 seed: Optional[int] = None, lanes: Optional[int] = None, num_beams: int = 1,
+                 length_penalty: float = 0.0) -> torch.Tensor:
         """Greedy (do_sample=False) or top-k/top-p sampling (do_sample=True; num_beams=1) decode
         -> codes [B, n] int64 on the device, finished rows padded with the stop token, n = steps until
         every row stopped (or max_new_tokens).  ``seed`` (default: drawn from torch's CPU generator)
-        keys the device RNG (by global row), so a fixed seed reproduces the draws for any lane split."""
+        keys the device RNG (by global row), so a fixed seed reproduces the draws for any lane split.
+        num_beams > 1: beam search / beam sample (``generate_beam``)."""
+        if num_beams and num_beams > 1:
+            assert forced_codes is None, "teacher forcing is a num_beams=1 test feature"
+            return self.generate_beam(conds, text_ids, max_new_tokens, num_beams, repetition_penalty,
+                                      length_penalty, min_new_tokens, do_sample, temperature, top_k, top_p, seed,
+                                      use_graph, check_every)
         emb, pad, s = self.prepare_inputs(conds, text_ids)
         B = emb.shape[0]
         assert s + 1 + max_new_tokens <= self.max_kv, "KV capacity exceeded"
@@ -448,9 +465,14 @@ class HipGPT:
                 ln["graph"] = (self._capture(st, min_new, penalty), gkey)
             ln["graph_ok"] = True
 
+    MUTABLE = ("t", "x", "h", "seen", "done", "codes")
+    BEAM_MUTABLE = ("beam_score", "kv_rows", "done_u", "hyp_score", "hyp_len", "hyp_codes", "hyp_n", "hyp_order",
+                    "hyp_worst")
+
     def _capture(self, st, min_new, penalty):
         """Capture one decode step into a hipGraph; counters are device-side so replays advance."""
-        saved = {k: st[k].clone() for k in ("t", "x", "h", "seen", "done", "codes")}
+        keys = self.MUTABLE + (self.BEAM_MUTABLE if "kv_rows" in st else ())
+        saved = {k: st[k].clone() for k in keys}
         cur = torch.cuda.current_stream(self.dev)
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(cur)
@@ -463,6 +485,162 @@ class HipGPT:
         with torch.cuda.graph(g):
             self._decode_step(st, min_new, penalty)
         return g  # capture does not execute the kernels; state is intact
+
+    # ---------------- beam search / beam sample (num_beams > 1) ----------------
+    def _beam_step(self, st, col_delta):
+        """candidates per row, then per-utterance selection + reorder + next embedding (gpt_beam.hip)."""
+        bm = st["beam"]
+        stream = _hip.stream_ptr()
+        R, K = st["B"], bm["K"]
+        smp = bm["sampling"]
+        _hip.check(self.lib.itts_beam_candidates(
+            st["logits"].data_ptr(), self.Vp, self.V, st["seen"].data_ptr(), st["beam_score"].data_ptr(),
+            st["t"].data_ptr(), col_delta, int(bm["min_new"]), self.stop_mel, float(bm["penalty"]), int(smp is not None),
+            float(smp[0]) if smp else 1.0, int(smp[1]) if smp else 0, float(smp[2]) if smp else 1.0, K,
+            st["cand_key"].data_ptr(), st["cand_score"].data_ptr(), st["cand_tok"].data_ptr(), R, stream),
+            "itts_beam_candidates")
+        ln1 = self.layers[0].ln1
+        _hip.check(self.lib.itts_beam_select(
+            st["cand_key"].data_ptr(), st["cand_score"].data_ptr(), st["cand_tok"].data_ptr(), K, self.V,
+            self.stop_mel, int(smp is not None), float(bm["length_penalty"]), st["t"].data_ptr(), col_delta,
+            st["done_u"].data_ptr(), st["beam_score"].data_ptr(), st["codes"].data_ptr(), st["max_new"],
+            st["seen"].data_ptr(), self.Vp, st["base_ids"].data_ptr(), st["base_ids"].numel(),
+            st["kv_rows"].data_ptr(), st["kv_rows"].stride(0), st["s"] + 1, st["hyp_score"].data_ptr(),
+            st["hyp_len"].data_ptr(), st["hyp_codes"].data_ptr(), st["hyp_n"].data_ptr(), st["hyp_order"].data_ptr(),
+            st["hyp_worst"].data_ptr(), self.mel_emb.data_ptr(), self.mel_pos.data_ptr(), 2, self.D,
+            ln1[0].data_ptr(), ln1[1].data_ptr(), st["x"].data_ptr(), st["h"].data_ptr(), _hip.dtype_code(st["h"]),
+            R // K, st["max_new"], stream), "itts_beam_select")
+
+    def _beam_state(self, B: int, K: int, max_new: int, s: int):
+        key = ("beam", B, K, max_new, s)
+        ln = self._lanes.get("beam")
+        if ln is None or ln["key"] != key:
+            if ln is not None:
+                self._lanes.pop("beam")
+                del ln
+                torch.cuda.empty_cache()
+            R = B * K
+            st = self._alloc_state(R, max_new)
+            dev = self.dev
+            st.update({
+                "beam_score": torch.zeros(R, device=dev),
+                "cand_key": torch.zeros(R, 2 * K, device=dev),
+                "cand_score": torch.zeros(R, 2 * K, device=dev),
+                "cand_tok": torch.zeros(R, 2 * K, dtype=torch.int32, device=dev),
+                "kv_rows": torch.zeros(R, self.max_kv, dtype=torch.int32, device=dev),
+                "done_u": torch.zeros(B, dtype=torch.uint8, device=dev),
+                "hyp_score": torch.zeros(B, K, device=dev),
+                "hyp_len": torch.zeros(B, K, dtype=torch.int32, device=dev),
+                "hyp_codes": torch.zeros(B, K, max_new, dtype=torch.int32, device=dev),
+                "hyp_n": torch.zeros(B, dtype=torch.int32, device=dev),
+                "hyp_order": torch.zeros(B, K, dtype=torch.int32, device=dev),
+                "hyp_worst": torch.zeros(B, device=dev),
+                "base_ids": torch.tensor([1, self.start_mel], dtype=torch.int32, device=dev),
+            })
+            ln = {"key": key, "st": st, "graph": None}
+            self._lanes["beam"] = ln
+        return ln
+
+    @torch.no_grad()
+    def generate_beam(self, conds: torch.Tensor, text_ids: torch.Tensor, max_new_tokens: int, num_beams: int = 3,
+                      repetition_penalty: float = 10.0, length_penalty: float = 0.0, min_new_tokens: int = 0,
+                      do_sample: bool = False, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
+                      seed: Optional[int] = None, use_graph: bool = True, check_every: int = 16) -> torch.Tensor:
+        """``generate(num_beams=K)`` of inference_speech (gpt/model.py:698-703) with transformers 4.36
+        ``beam_search`` (do_sample=False) / ``beam_sample`` (do_sample=True) semantics -- the
+        reference's default decoding (infer.py:535-543).  Rows r = b*K + k; the prompt is prefilled
+        once per utterance (cache row b*K) and shared through the KV lineage table.
+        -> codes [B, n] int64 (best hypothesis, then the stop token, padded with it)."""
+        K = int(num_beams)
+        assert 2 <= K <= 8, "num_beams must be in [2, 8]"
+        emb, pad, s = self.prepare_inputs(conds, text_ids)
+        B = emb.shape[0]
+        R = B * K
+        assert s + 1 + max_new_tokens <= self.max_kv, "KV capacity exceeded"
+        sampling = (float(temperature), int(top_k), float(top_p)) if do_sample else None
+        if do_sample and seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        ln = self._beam_state(B, K, max_new_tokens, s)
+        st = ln["st"]
+        st["s"] = s
+        st["beam"] = {"K": K, "sampling": sampling, "min_new": min_new_tokens, "penalty": repetition_penalty,
+                      "length_penalty": length_penalty}
+        rows_b = torch.arange(B, device=self.dev).repeat_interleave(K)
+        st["pad"].copy_(pad[rows_b])
+        st["seen"].zero_()
+        st["seen"][:, 1] = 1
+        st["seen"][:, self.start_mel] = 1
+        st["done"].zero_()
+        st["done_u"].zero_()
+        st["codes"].fill_(self.stop_mel)
+        bs = torch.zeros(B, K, device=self.dev)
+        if not do_sample:
+            bs[:, 1:] = -1e9  # HF 4.36 beam_search: only beam 0 expands at the first step
+        st["beam_score"].copy_(bs.view(-1))
+        st["kv_rows"].copy_((rows_b * K).int()[:, None].expand(R, self.max_kv))
+        st["hyp_n"].zero_()
+        st["hyp_worst"].fill_(1e9)
+        sd = [0, 0] if seed is None else [(seed >> 32 * i) & 0xFFFFFFFF for i in range(2)]
+        sd = [v - (1 << 32) if v >= 1 << 31 else v for v in sd]
+        st["t"].copy_(torch.tensor([0, 0, sd[0], sd[1]], dtype=torch.int32))
+        # ---- prefill of the B prompts into cache rows b*K ----
+        M = B * (s + 1)
+        x = emb.reshape(M, self.D).contiguous()
+        starts = torch.arange(B, dtype=torch.int32, device=self.dev) * (s + 1)
+        lens = torch.full((B,), s + 1, dtype=torch.int32, device=self.dev)
+        self._forward_rows(x, starts, lens, pad, s + 1, cache=(st["kc"][:, ::K], st["vc"][:, ::K]))
+        last = (starts + s)[rows_b].contiguous()
+        self._ln(x, st["h"], self.ln_f, self.final_norm, idx=last, M=R)
+        if self.mode == "f32":
+            self._gemm(st["h"][:R], self.head_w, st["logits"], bias=self.head_b)
+        else:
+            self._dg(st["h"], self.head_w, R, self.head_b, st["logits"])
+        self._beam_step(st, 0)
+        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling)
+        graph_ok = use_graph and max_new_tokens > 1
+        if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
+            ln["graph"] = (self._capture(st, min_new_tokens, repetition_penalty), gkey)
+        steps = 1
+        while steps < max_new_tokens:
+            if graph_ok:
+                ln["graph"][0].replay()
+            else:
+                self._decode_step(st, min_new_tokens, repetition_penalty)
+            steps += 1
+            if steps % check_every == 0 and bool(st["done_u"].all()):
+                break
+        return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
+
+    def _beam_finalize(self, st, B, K, steps, max_new, length_penalty):
+        """BeamSearchScorer.finalize: open beams of unfinished utterances become hypotheses (generated
+        length = steps); the best hypothesis per utterance, then eos, padded (HF beam_search.py)."""
+        done = st["done_u"].cpu().numpy()
+        hs, hl = st["hyp_score"].cpu().numpy(), st["hyp_len"].cpu().numpy()
+        hc, hn, ho = st["hyp_codes"].cpu().numpy(), st["hyp_n"].cpu().numpy(), st["hyp_order"].cpu().numpy()
+        hw = st["hyp_worst"].cpu().numpy()
+        codes = st["codes"][:, :steps].cpu().numpy()
+        scores = st["beam_score"].cpu().numpy()
+        best = []
+        for b in range(B):
+            hyps = [(float(hs[b, ho[b, i]]), list(hc[b, ho[b, i], : hl[b, ho[b, i]]])) for i in range(hn[b])]
+            worst = float(hw[b])
+            if not done[b]:
+                for k in range(K):
+                    sc = float(scores[b * K + k]) / (steps ** length_penalty)
+                    if len(hyps) < K or sc > worst:
+                        hyps.append((sc, list(codes[b * K + k])))
+                        if len(hyps) > K:
+                            order = sorted((h[0], i) for i, h in enumerate(hyps))
+                            del hyps[order[0][1]]
+                            worst = order[1][0]
+                        else:
+                            worst = min(sc, worst)
+            best.append(sorted(hyps, key=lambda h: h[0])[-1][1])
+        n = min(max(len(t) for t in best) + 1, max_new)
+        out = torch.full((B, n), self.stop_mel, dtype=torch.long)
+        for b, t in enumerate(best):
+            out[b, : len(t)] = torch.tensor(t, dtype=torch.long)
+        return out.to(self.dev)
 
     # ---------------- latent pass ----------------
     @torch.no_grad()

@@ -15,10 +15,10 @@ What differs is underneath:
   the constructor raises (the reference fell back to torch, infer.py:97-109);
 * decoding: greedy (``do_sample=False, num_beams=1``) reproduces the reference's ids exactly (f32);
   ``do_sample=True`` runs the Temperature/TopK/TopP warpers + multinomial draw on the GPU with a
-  device RNG (same distribution, different draws than torch -- statistical parity).  Beam search
-  (``num_beams > 1``, the reference default) is not implemented yet: it is decoded with
-  ``num_beams=1`` and a RuntimeWarning.  An extra ``seed=`` generation
-  kwarg fixes the device RNG.
+  device RNG (same distribution, different draws than torch -- statistical parity).  ``num_beams > 1``
+  (the reference default: beam sample, 3 beams) runs HF 4.36 beam_search / beam_sample on the GPU
+  (gpt_beam.hip; beam search ids bit-exact in f32 mode, beam sample statistical).  An extra ``seed=``
+  generation kwarg fixes the device RNG.
 """
 from __future__ import annotations
 
@@ -185,7 +185,7 @@ class IndexTTS:
         top_p = kw.pop("top_p", 0.8)
         top_k = kw.pop("top_k", 30)
         temperature = kw.pop("temperature", 1.0)
-        kw.pop("length_penalty", 0.0)  # only meaningful for beam search
+        length_penalty = kw.pop("length_penalty", 0.0)
         num_beams = kw.pop("num_beams", 3)
         repetition_penalty = kw.pop("repetition_penalty", 10.0)
         max_mel_tokens = kw.pop("max_mel_tokens", max_tok_default)
@@ -194,15 +194,17 @@ class IndexTTS:
         kw.pop("num_return_sequences", None)
         if kw:
             warnings.warn(f"ignored generation kwargs: {sorted(kw)}", RuntimeWarning)
-        if num_beams and num_beams > 1:
-            warnings.warn(f"num_beams={num_beams}: beam search is not implemented on the HIP path yet; "
-                          "decoding with num_beams=1", RuntimeWarning)
+        num_beams = int(num_beams or 1)
+        if num_beams > 8:
+            raise ValueError("HIP beam search supports num_beams <= 8")
         smp = {}
+        if num_beams > 1:
+            smp = dict(num_beams=num_beams, length_penalty=float(length_penalty or 0.0))
         if do_sample:
             top_k = int(top_k or 0)
             if top_k > 64 or (top_k == 0 and top_p is not None and top_p < 1.0):
                 raise ValueError("HIP sampler supports 1 <= top_k <= 64 (or top_k=0 with top_p=1)")
-            smp = dict(do_sample=True, temperature=float(temperature), top_k=top_k,
+            smp.update(do_sample=True, temperature=float(temperature), top_k=top_k,
                        top_p=1.0 if top_p is None else float(top_p), seed=seed)
         return dict(max_mel_tokens=int(max_mel_tokens), repetition_penalty=float(repetition_penalty),
                     min_new_tokens=int(min_new_tokens), **smp)

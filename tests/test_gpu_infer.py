@@ -128,11 +128,18 @@ def test_infer_matches_oracle_chain(ckpt, tts, tmp_path, fast):
 
 def test_infer_reference_defaults_run(ckpt, tts):
     """srt_dubbing calls infer(text=, audio_prompt=, output_path=None) with the reference defaults
-    (beam-sample, num_beams=3): runs (beam search decoded as num_beams=1, warned)."""
-    with pytest.warns(RuntimeWarning, match="num_beams"):
+    (beam-sample: do_sample=True, num_beams=3, top_k 30, top_p 0.8): decoded by the HIP beam kernels,
+    no decoding-mode warning, reproducible for a fixed seed."""
+    import warnings
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
         sr, got = tts.infer(text="Mind the gap.", audio_prompt=str(ckpt[0] / "prompt.wav"), output_path=None,
                             max_mel_tokens=24, seed=1)
+    assert not [w for w in rec if "num_beams" in str(w.message) or "ignored generation" in str(w.message)]
     assert sr == 24000 and got.shape[0] > 0 and got.shape[0] % 1024 == 0
+    _, again = tts.infer(text="Mind the gap.", audio_prompt=str(ckpt[0] / "prompt.wav"), output_path=None,
+                         max_mel_tokens=24, seed=1)
+    np.testing.assert_array_equal(again, got)
 
 
 # ------------------------------------------------------------------ sampling kernel

@@ -137,9 +137,14 @@ def test_decoding_kwargs():
     with warnings.catch_warnings(record=True) as w:
         warnings.simplefilter("always")
         d = IndexTTS._decoding({})  # reference defaults: beam-sample, num_beams=3
-    assert any("num_beams=3" in str(x.message) for x in w)
-    assert d == dict(max_mel_tokens=600, repetition_penalty=10.0, min_new_tokens=0, do_sample=True,
-                     temperature=1.0, top_k=30, top_p=0.8, seed=None)
+    assert not w
+    assert d == dict(max_mel_tokens=600, repetition_penalty=10.0, min_new_tokens=0, num_beams=3,
+                     length_penalty=0.0, do_sample=True, temperature=1.0, top_k=30, top_p=0.8, seed=None)
+    b = IndexTTS._decoding(dict(do_sample=False, num_beams=2, length_penalty=1.0))
+    assert b == dict(max_mel_tokens=600, repetition_penalty=10.0, min_new_tokens=0, num_beams=2,
+                     length_penalty=1.0)
+    with pytest.raises(ValueError):
+        IndexTTS._decoding(dict(num_beams=9))
     g = IndexTTS._decoding(dict(do_sample=False, num_beams=1, max_mel_tokens=64))
     assert g == dict(max_mel_tokens=64, repetition_penalty=10.0, min_new_tokens=0)
     with pytest.raises(ValueError):
