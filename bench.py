@@ -145,6 +145,9 @@ def main():
     ap.add_argument("--cpu-codes", type=int, default=96)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="run the K timed batches through BatchedTTS.synthesize_many (decode of batch i+1 "
+                         "overlapped with the latent pass + vocoder of batch i)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,8 +192,16 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     audio = 0.0
-    for _ in range(args.steps):
-        audio += step()
+    if args.pipeline:
+        res = tts.synthesize_many([(mels, texts)] * args.steps, max_mel_tokens=N, min_new_tokens=N)
+        torch.cuda.synchronize()
+        for pcm, lens, _ in res:
+            if world > 1:
+                gather_waveforms([pcm[b, : int(lens[b])] for b in range(B)], B * world, dev)
+            audio += float(lens.sum()) / SR
+    else:
+        for _ in range(args.steps):
+            audio += step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

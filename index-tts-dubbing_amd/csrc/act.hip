@@ -172,7 +172,9 @@ extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, 
   ITTS_REQUIRE((dtype_in == ITTS_F32 || dtype_in == ITTS_BF16) && (dtype_out == ITTS_F32 || dtype_out == ITTS_BF16),
                fn, "unsupported dtype (f32=0, bf16=1)");
   ActArgs a{x, y, up12, down12, log_alpha, log_beta, lengths, B, C, T, 0, 0, x_sb, x_st, x_sc, y_sb, y_st, y_sc};
-  a.CT = C < 64 ? C : 64;
+  // channel tile: all channels when C <= 64, else 64 -- or 32 when 32 divides C and 64 does not
+  // (C = 96: two 64-channel tiles would leave half the second tile's threads idle)
+  a.CT = C <= 64 ? C : (C % 64 != 0 && C % 32 == 0 ? 32 : 64);
   a.nsub = kThreads / a.CT;
   hipStream_t s = itts::as_stream(stream);
   // vectorised staging: channel-last bf16 input, 16-B aligned rows

@@ -23,6 +23,16 @@
 namespace {
 
 constexpr int kMaxTapsAc = 16;
+// output rows per workgroup by padded channel count (tuning: -DITTS_AMP_TT32=... etc.)
+#ifndef ITTS_AMP_TT32
+#define ITTS_AMP_TT32 256
+#endif
+#ifndef ITTS_AMP_TT64
+#define ITTS_AMP_TT64 256
+#endif
+#ifndef ITTS_AMP_TT96
+#define ITTS_AMP_TT96 128
+#endif
 constexpr int kSpan = 64;  // max (max_off - min_off) of the taps
 
 struct AcArgs {
@@ -378,9 +388,9 @@ extern "C" int itts_amp_conv_fwd(const void* x, int64_t x_sb, int64_t ldx, const
   ITTS_REQUIRE(hi - lo <= kSpan, fn, "tap span exceeds 64 rows");
   hipStream_t s = itts::as_stream(stream);
   const int ci = (Cin + 31) / 32 * 32, co = (Cout + 31) / 32 * 32;
-  if (ci == 32 && co == 32) launch_ac<32, 32, 256>(a, s);
-  else if (ci == 64 && co == 64) launch_ac<64, 64, 128>(a, s);
-  else if (ci == 96 && co == 96) launch_ac<96, 96, 128>(a, s);
+  if (ci == 32 && co == 32) launch_ac<32, 32, ITTS_AMP_TT32>(a, s);
+  else if (ci == 64 && co == 64) launch_ac<64, 64, ITTS_AMP_TT64>(a, s);
+  else if (ci == 96 && co == 96) launch_ac<96, 96, ITTS_AMP_TT96>(a, s);
   else return itts::fail(fn, "supported (Cin, Cout) padded pairs: (32,32), (64,64), (96,96)");
   return itts::check_launch(fn);
 }

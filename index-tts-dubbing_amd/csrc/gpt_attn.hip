@@ -49,8 +49,14 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 // ROWS (beam search): key position p of sequence b lives in cache row kv_rows[b * ld_rows + p] (beams
 // share their common prefix, HF's per-step cache reorder becomes this lineage table); this step's
 // key/value go to the sequence's own row b.
+#ifndef ITTS_ATTN_KB
+#define ITTS_ATTN_KB 8
+#endif
+#ifndef ITTS_ATTN_WPS
+#define ITTS_ATTN_WPS 1
+#endif
 template <typename TC, typename TO, int NT, bool ROWS>
-__global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
+__global__ __launch_bounds__(NT, ITTS_ATTN_WPS) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
                                                          int64_t split_stride, const float* __restrict__ qkv_bias,
                                                          TC* __restrict__ cache_k, TC* __restrict__ cache_v,
                                                          int64_t cache_bs, int64_t cache_hs, const int32_t* pad,
@@ -58,7 +64,7 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(const float* __restrict
                                                          TO* __restrict__ out, int64_t ldo, int H,
                                                          const int32_t* __restrict__ kv_rows, int64_t ld_rows) {
   constexpr int NG = NT / 8;
-  constexpr int KB = 8;                          // keys per group per round (packed rows in registers)
+  constexpr int KB = ITTS_ATTN_KB;               // keys per group per round (packed rows in registers)
   constexpr int RW = sizeof(TC) * 8 / 16;       // 16-B vectors per lane per row (bf16: 1, f32: 2)
   __shared__ float qs[kHD], kn[kHD], vn[kHD];
   __shared__ float gm[NG], gl[NG];

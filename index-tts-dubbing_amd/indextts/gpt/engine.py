@@ -16,6 +16,7 @@ done flags, codes) lives on the device so one captured hipGraph replays every st
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -106,8 +107,9 @@ class HipGPT:
     # ---------------- conditioning + inputs ----------------
     @torch.no_grad()
     def conditioning(self, mel: torch.Tensor, mel_lengths=None) -> torch.Tensor:
-        return get_conditioning(self.sd_cond, self.cfg, mel.to(self.dev).float(),
-                                None if mel_lengths is None else mel_lengths.to(self.dev))
+        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):  # run-to-run identical
+            return get_conditioning(self.sd_cond, self.cfg, mel.to(self.dev).float(),
+                                    None if mel_lengths is None else mel_lengths.to(self.dev))
 
     def prepare_inputs(self, conds: torch.Tensor, text_ids: torch.Tensor):
         """``prepare_gpt_inputs`` (gpt/model.py:591-654): strip ids 0/1, [0]+ids+[1], left zero pad.
@@ -200,7 +202,7 @@ class HipGPT:
             "qkv": torch.zeros(self.KSPLIT["qkv"] * B * 3 * D, device=dev),  # c_attn split-K slabs [split][B][3D]
             "o": torch.zeros(Mp, D, dtype=ad, device=dev),
             "f": torch.zeros(Mp, 4 * D, dtype=ad, device=dev),
-            "ws": torch.zeros(8 * B * D, device=dev),  # split-K partial products [split][B][D]
+            "ws": torch.zeros(max(8, self.KSPLIT["o"], self.KSPLIT["proj"]) * B * D, device=dev),  # split-K partials [split][B][D]
             "logits": torch.zeros(B, self.Vp, device=dev),  # row pitch Vp (16-B aligned rows)
             "kc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
             "vc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
@@ -287,8 +289,11 @@ class HipGPT:
             self._sample(st, 1, min_new, penalty)
         _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
-    # split-K factors of the residual projections (partials reduced by itts_residual_reduce_ln)
+    # split-K factors of the residual projections (partials reduced by itts_residual_reduce_ln);
+    # ITTS_KSPLIT="qkv,o,proj" overrides them (tuning sweeps)
     KSPLIT = {"qkv": 2, "o": 2, "proj": 8}
+    if os.environ.get("ITTS_KSPLIT"):
+        KSPLIT = dict(zip(("qkv", "o", "proj"), (int(v) for v in os.environ["ITTS_KSPLIT"].split(","))))
 
     @staticmethod
     def _ksplit(K, want):

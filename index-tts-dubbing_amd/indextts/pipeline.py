@@ -161,3 +161,48 @@ class BatchedTTS:
         _, pcm = self.vocoder.forward(latent, lens, spk)
         mark("vocoder")
         return pcm, (lens.long() * HOP), fixed
+
+    @torch.no_grad()
+    def synthesize_many(self, batches: Sequence[tuple], max_mel_tokens: int = 600, repetition_penalty: float = 10.0,
+                        min_new_tokens: int = 0, keys=None, front_priority: int = -1, streams=None, **sampling):
+        """Pipelined ``synthesize`` over several batches [(mels, texts), ...]: the front half (prompt
+        features, GPT decode, remove_long_silence) of batch i+1 runs on a high-priority stream while
+        the back half (latent pass + vocoder) of batch i runs on a second stream.  The decode step is a
+        latency-bound chain of small kernels that leaves most CUs idle; the vocoder's MFMA/HBM-heavy
+        launches fill them.  Every batch's results are identical to ``synthesize`` (same kernels,
+        same per-row math; only the launch interleaving differs).
+        -> list of (pcm int16 [B, Tmax] (device), sample lengths [B] (cpu), codes list); synchronise
+        the device (or the current stream) before reading pcm."""
+        dev = self.device
+        cur = torch.cuda.current_stream(dev)
+        if streams is not None:  # caller-made streams (e.g. a CU-masked back stream)
+            front, back = streams
+        else:
+            front = torch.cuda.Stream(dev, priority=front_priority)
+            back = torch.cuda.Stream(dev)
+        front.wait_stream(cur)
+        back.wait_stream(cur)
+        keep, out = [], []
+        for bi, (mels, texts) in enumerate(batches):
+            B = len(texts)
+            with torch.cuda.stream(front):
+                conds, spk = self.prompt_features(mels, None if keys is None else keys[bi])
+                L = max(int(t.numel()) for t in texts)
+                ids = torch.full((B, L), self.stop_text, dtype=torch.long)
+                for b, t in enumerate(texts):
+                    ids[b, : t.numel()] = t.reshape(-1).long()
+                codes = self.gpt.generate(conds, ids.to(dev), max_mel_tokens, repetition_penalty=repetition_penalty,
+                                          min_new_tokens=min_new_tokens, **sampling)
+                rows = codes.cpu().numpy()  # syncs the front stream only
+            fixed = [torch.from_numpy(remove_long_silence(rows[b], self.stop)) for b in range(B)]
+            fixed = [f if f.numel() > 0 else torch.tensor([self.stop]) for f in fixed]
+            back.wait_stream(front)
+            with torch.cuda.stream(back):
+                latent, lens = self.gpt.latent(conds, [t.reshape(-1) for t in texts], fixed)
+                _, pcm = self.vocoder.forward(latent, lens, spk)
+            keep.append((conds, spk, codes, latent))  # alive until both streams are past them
+            out.append((pcm, lens.long() * HOP, fixed))
+        cur.wait_stream(back)
+        cur.wait_stream(front)
+        self._pipeline_keep = keep  # released by the next call (the caller synchronises before reuse)
+        return out

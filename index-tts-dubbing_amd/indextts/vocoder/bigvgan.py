@@ -18,6 +18,7 @@ PyTorch ops on the device and cached by the caller (quirk Q6).
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List
 
 import numpy as np
@@ -119,6 +120,9 @@ class HipBigVGAN:
     #   (the fused form ties the igemm path there, the split form beats both);  others: act + igemm
     FUSED_CHANNELS = (24, 48)
     SPLIT_CHANNELS = (96,)
+    if os.environ.get("ITTS_VOC_FUSED") is not None:  # tuning sweeps: "24,48,96"
+        FUSED_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_FUSED"].split(",") if v)
+        SPLIT_CHANNELS = tuple(sorted({24, 48, 96} - set(FUSED_CHANNELS)))
 
     def __init__(self, state_dict, cfg_bv, device="cuda"):
         self.lib = _hip.load()
@@ -165,8 +169,10 @@ class HipBigVGAN:
     # ---------------- per-prompt (cached by the caller) ----------------
     @torch.no_grad()
     def speaker(self, mel_ref: torch.Tensor) -> torch.Tensor:
-        """mel_ref [B, T, n_mels] -> [B, spk_dim] (ECAPA; PyTorch ops on the device)."""
-        return speaker_embedding(self.sd_torch, mel_ref.to(self.device).float())
+        """mel_ref [B, T, n_mels] -> [B, spk_dim] (ECAPA; PyTorch ops on the device).  MIOpen is
+        asked for deterministic conv algorithms: the default choice varies by ~4e-6 run to run."""
+        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
+            return speaker_embedding(self.sd_torch, mel_ref.to(self.device).float())
 
     @torch.no_grad()
     def cond_biases(self, spk: torch.Tensor):
