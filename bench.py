@@ -145,6 +145,11 @@ def main():
     ap.add_argument("--cpu-codes", type=int, default=96)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
+    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c3",
+                    help="BASELINE.json configs: c3 (default, the metric's config: batch 32 per GPU), c2 (one "
+                         "utterance), c5 (srt_dubbing long-form: a synthetic SRT of --cues cues sharded over the "
+                         "ranks, length-bucketed chunks of 32 streamed through the pipelined driver)")
+    ap.add_argument("--cues", type=int, default=256)
     ap.add_argument("--pipeline", action="store_true",
                     help="run the K timed batches through BatchedTTS.synthesize_many (decode of batch i+1 "
                          "overlapped with the latent pass + vocoder of batch i)")
@@ -166,7 +171,11 @@ def main():
     cfg = load_config(default_config_path())
     gsd = gpt_state_dict(cfg.gpt, seed=0, mel_head_std=0.08)
     vsd = bigvgan_state_dict(cfg.bigvgan, seed=0)
+    if args.workload == "c2":
+        args.batch = 1
     B, N, L = args.batch, args.codes, args.text_len
+    if args.workload == "c5":
+        return long_form(args, cfg, gsd, vsd, dev, world, rank)
     tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + L + 2 + 1 + N + 8)
     timer = KernelTimer()
     install_conv_timer(tts.vocoder, timer)
@@ -251,15 +260,92 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic: seeded random-init IndexTTS-1.5 weights, random 511-frame prompt mels, random text ids",
-        "config": {"workload": f"C3: batch={B} zero-shot utterances per GPU (one prompt each), L={L} text ids, "
+        "config": {"workload": f"{'C2' if args.workload == 'c2' else 'C3'}: batch={B} zero-shot utterance"
+                               f"{'s' if B > 1 else ''} per GPU (one prompt each), L={L} text ids, "
                                f"{N} codes each (EOS suppressed): conditioning+ECAPA, GPT prefill+decode (hipGraph), "
-                               "latent pass, BigVGAN2 -> int16", "global_batch": B * world, "seq_len": N,
-                   "parallelism": f"dp{world}"},
+                               "latent pass, BigVGAN2 -> int16" + (", pipelined batches" if args.pipeline else ""),
+                   "global_batch": B * world, "seq_len": N, "parallelism": f"dp{world}"},
         "roofline": dec,
         "roofline_vocoder_conv": voc,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def long_form(args, cfg, gsd, vsd, dev, world, rank):
+    """C5 (BASELINE.json configs[4]): srt_dubbing long-form.  A synthetic SRT of args.cues cues (seed 3),
+    cue text L ~ U[8, 96], one shared prompt (features computed once, cached by key); cue i runs on rank
+    i % world; each rank sorts its cues by length into chunks of 32 (texts padded to the chunk's bucket
+    with the stop id 1, which prepare_gpt_inputs strips: per-cue results are unchanged), 6 codes per
+    text token of the bucket (EOS suppressed), and streams the chunks through the pipelined driver;
+    the finished waveforms are gathered to rank 0.  One step = the whole SRT."""
+    from indextts.pipeline import BatchedTTS, SR
+    from indextts.sharding import gather_waveforms, shard
+    g = np.random.default_rng(3)
+    n_cues = args.cues
+    lens_all = g.integers(8, 97, n_cues)
+    texts_all = [torch.from_numpy(g.integers(2, int(cfg.gpt.number_text_tokens), int(n)).astype(np.int64))
+                 for n in lens_all]
+    mel = torch.from_numpy(g.normal(-4.0, 2.0, (1, 100, args.prompt_frames)).astype(np.float32)).to(dev)
+    buckets = (32, 64, 96)
+    tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + 96 + 2 + 1 + 6 * 96 + 8)
+    mine = sorted(shard(n_cues, world, rank), key=lambda i: -int(lens_all[i]))
+    batches, keys, order = [], [], []
+    for c in range(0, len(mine), 32):
+        idx = mine[c: c + 32]
+        order += idx
+        bl = next(b for b in buckets if b >= max(int(lens_all[i]) for i in idx))
+        tx = [torch.cat([texts_all[i], torch.ones(bl - len(texts_all[i]), dtype=torch.int64)]).to(dev) for i in idx]
+        batches.append(([mel] * len(idx), tx, {"max_mel_tokens": 6 * bl, "min_new_tokens": 6 * bl}))
+        keys.append([("prompt", 0)] * len(idx))
+
+    def step():
+        res = tts.synthesize_many(batches, keys=keys)
+        torch.cuda.synchronize()
+        audio = 0.0
+        by_cue = {}
+        it = iter(order)
+        for pcm, lens, _ in res:
+            for b in range(pcm.shape[0]):
+                by_cue[next(it)] = pcm[b, : int(lens[b])]
+            audio += float(lens.sum()) / SR
+        if world > 1:  # in this rank's shard order
+            gather_waveforms([by_cue[i] for i in shard(n_cues, world, rank)], n_cues, dev)
+        return audio
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    audio = 0.0
+    for _ in range(args.steps):
+        audio += step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+        a = torch.tensor([audio], device=dev, dtype=torch.float64)
+        dist.all_reduce(a, op=dist.ReduceOp.SUM)
+        audio = float(a)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(audio / dt, 3), "unit": "audio-seconds/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic: seeded random-init IndexTTS-1.5 weights, one random 511-frame prompt mel, "
+                    "random cue text ids",
+            "config": {"workload": f"C5: srt long-form, {n_cues} cues (L ~ U[8,96]) sharded over {world} GPU(s), "
+                                   "length-bucketed chunks of 32 (buckets 32/64/96 text ids, 6 codes per id: <= 600 = max_mel_tokens), "
+                                   "pipelined decode || latent+vocoder, RCCL gather",
+                       "global_batch": n_cues, "seq_len": None, "parallelism": f"dp{world}"}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

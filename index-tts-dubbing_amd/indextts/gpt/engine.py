@@ -340,19 +340,23 @@ class HipGPT:
         step = (B + n - 1) // n
         return [(r, min(B, r + step)) for r in range(0, B, step)]
 
+    MAX_CACHED_SHAPES = 4  # decode states (+ captured graphs) kept per lane, LRU
+
     def _lane(self, i: int, rows: int, max_new: int, s: int):
+        """decode state + captured graph for lane i at this (rows, max_new, prompt length) shape; a few
+        shapes stay cached so that alternating bucket shapes (long-form driver) do not re-capture."""
         lanes = self.__dict__.setdefault("_lanes", {})
-        ln = lanes.get(i)
         key = (rows, max_new, s)
-        if ln is None or ln["key"] != key:
-            if ln is not None:  # free the old lane before allocating (KV caches can be large)
-                lanes.pop(i)
-                del ln
+        ln = lanes.pop((i, key), None)
+        if ln is None:
+            mine = [k for k in lanes if isinstance(k, tuple) and len(k) == 2 and k[0] == i and isinstance(k[1], tuple)]
+            if len(mine) >= self.MAX_CACHED_SHAPES:  # evict the least recently used shape first
+                del lanes[mine[0]]
                 torch.cuda.empty_cache()
             ln = {"key": key, "st": self._alloc_state(rows, max_new), "graph": None,
                   "stream": lanes.get(("stream", i)) or torch.cuda.Stream(self.dev)}
             lanes[("stream", i)] = ln["stream"]
-            lanes[i] = ln
+        lanes[(i, key)] = ln  # (re)inserted last = most recently used
         return ln
 
     @torch.no_grad()

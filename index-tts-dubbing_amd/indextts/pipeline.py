@@ -165,7 +165,8 @@ class BatchedTTS:
     @torch.no_grad()
     def synthesize_many(self, batches: Sequence[tuple], max_mel_tokens: int = 600, repetition_penalty: float = 10.0,
                         min_new_tokens: int = 0, keys=None, front_priority: int = -1, streams=None, **sampling):
-        """Pipelined ``synthesize`` over several batches [(mels, texts), ...]: the front half (prompt
+        """Pipelined ``synthesize`` over several batches [(mels, texts[, {"max_mel_tokens": n,
+        "min_new_tokens": m}]), ...]: the front half (prompt
         features, GPT decode, remove_long_silence) of batch i+1 runs on a high-priority stream while
         the back half (latent pass + vocoder) of batch i runs on a second stream.  The decode step is a
         latency-bound chain of small kernels that leaves most CUs idle; the vocoder's MFMA/HBM-heavy
@@ -183,7 +184,9 @@ class BatchedTTS:
         front.wait_stream(cur)
         back.wait_stream(cur)
         keep, out = [], []
-        for bi, (mels, texts) in enumerate(batches):
+        for bi, batch in enumerate(batches):
+            mels, texts = batch[0], batch[1]
+            over = batch[2] if len(batch) > 2 else {}  # per-batch max_mel_tokens / min_new_tokens
             B = len(texts)
             with torch.cuda.stream(front):
                 conds, spk = self.prompt_features(mels, None if keys is None else keys[bi])
@@ -191,8 +194,9 @@ class BatchedTTS:
                 ids = torch.full((B, L), self.stop_text, dtype=torch.long)
                 for b, t in enumerate(texts):
                     ids[b, : t.numel()] = t.reshape(-1).long()
-                codes = self.gpt.generate(conds, ids.to(dev), max_mel_tokens, repetition_penalty=repetition_penalty,
-                                          min_new_tokens=min_new_tokens, **sampling)
+                codes = self.gpt.generate(conds, ids.to(dev), over.get("max_mel_tokens", max_mel_tokens),
+                                          repetition_penalty=repetition_penalty,
+                                          min_new_tokens=over.get("min_new_tokens", min_new_tokens), **sampling)
                 rows = codes.cpu().numpy()  # syncs the front stream only
             fixed = [torch.from_numpy(remove_long_silence(rows[b], self.stop)) for b in range(B)]
             fixed = [f if f.numel() > 0 else torch.tensor([self.stop]) for f in fixed]
