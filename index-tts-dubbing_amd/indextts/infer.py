@@ -303,6 +303,51 @@ class IndexTTS:
                                 generation_kwargs, fast=False)
 
 
+    def infer_many(self, audio_prompt, texts, output_paths=None, verbose=False, max_text_tokens_per_sentence=120,
+                   **generation_kwargs):
+        """Long-form / many-cue entry point (not in the reference): ``infer`` for every
+        text in ``texts`` with one shared prompt, all sentences of all texts batched together
+        (length-sorted chunks of MAX_BATCH) and streamed through the pipelined driver
+        (``BatchedTTS.synthesize_many``: GPT decode of chunk i+1 overlapped with the latent pass +
+        vocoder of chunk i).  Per text the result equals ``infer(audio_prompt, text, output_path,
+        ...)`` -- a path (wav written) or ``(24000, int16 [T, 1])``; returns the list in order."""
+        paths = list(output_paths) if output_paths is not None else [None] * len(texts)
+        assert len(paths) == len(texts), "one output path (or None) per text"
+        t0 = time.perf_counter()
+        cond_mel = self._prompt(audio_prompt)
+        dec = self._decoding(dict(generation_kwargs))
+        sent_ids, owner = [], []
+        for ti, text in enumerate(texts):
+            sentences = self.tokenizer.split_sentences(self.tokenizer.tokenize(text), max_text_tokens_per_sentence)
+            for sent in sentences:
+                sent_ids.append(torch.tensor(self.tokenizer.convert_tokens_to_ids(sent), dtype=torch.int32))
+                owner.append(ti)
+        order = sorted(range(len(sent_ids)), key=lambda i: -len(sent_ids[i]))
+        batches, chunks = [], []
+        keys = []
+        for c0 in range(0, len(order), self.MAX_BATCH):
+            idx = order[c0: c0 + self.MAX_BATCH]
+            chunks.append(idx)
+            batches.append(([cond_mel] * len(idx), [sent_ids[i].to(self.device) for i in idx]))
+            keys.append([("prompt", self.cache_audio_prompt)] * len(idx))
+        rows = [None] * len(sent_ids)
+        self._hit_limit = False
+        if batches:
+            res = self.engine.synthesize_many(batches, keys=keys, **dec)
+            torch.cuda.synchronize(self.device)
+            for idx, (pcm, n, _) in zip(chunks, res):
+                pcm = pcm.cpu()
+                for j, i in enumerate(idx):
+                    rows[i] = pcm[j, : int(n[j])]
+        if verbose:
+            print(f">> infer_many: {len(texts)} texts, {len(sent_ids)} sentences, {len(batches)} chunks")
+        out = []
+        for ti in range(len(texts)):
+            mine = [rows[i] for i in range(len(sent_ids)) if owner[i] == ti]
+            out.append(self._finish(mine, paths[ti], t0, cond_mel.shape[-1]))
+        return out
+
+
 if __name__ == "__main__":  # pragma: no cover
     from .cli import main
     sys.exit(main())

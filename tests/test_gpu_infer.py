@@ -220,3 +220,19 @@ def test_engine_sampling_seeded_and_graph_equals_eager(golden):
     assert not torch.equal(a[0], a[1])  # rows draw independently
     greedy = eng.generate(conds, text, 48, use_graph=True)
     assert torch.equal(greedy[0], greedy[1])
+
+
+def test_infer_many_equals_infer_per_text(ckpt, tts, tmp_path):
+    """long-form entry point: every text's result equals ``infer`` on it alone (greedy, f32)."""
+    texts = ["Mind the gap.", TEXT, "", "Please stand clear of the closing doors."]
+    gen = dict(do_sample=False, num_beams=1, max_mel_tokens=24)
+    prompt = str(ckpt[0] / "prompt.wav")
+    got = tts.infer_many(prompt, texts, max_text_tokens_per_sentence=12, **gen)
+    assert len(got) == len(texts)
+    for t, g in zip(texts, got):
+        sr, want = tts.infer(prompt, t, None, max_text_tokens_per_sentence=12, **gen)
+        assert g[0] == sr == 24000
+        np.testing.assert_array_equal(g[1], want)
+    paths = [str(tmp_path / f"c{i}.wav") for i in range(len(texts))]
+    assert tts.infer_many(prompt, texts, paths, max_text_tokens_per_sentence=12, **gen) == paths
+    np.testing.assert_array_equal(_read_wav(paths[1]), got[1][1][:, 0])
