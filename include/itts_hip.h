@@ -81,6 +81,16 @@ int itts_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* w
                         const int32_t* lengths, int B, int Tmax, float* wav, int16_t* pcm, int64_t y_sb,
                         int dtype_in, void* stream);
 
+/* ---- prompt front-end ------------------------------------------------------------------------- */
+
+/* log-mel spectrogram of B prompts (audio f32 [B][ld_audio], L samples each): center reflect padding
+ * by n_fft/2, hop, caller's window [n_fft] (periodic Hann), |STFT| (power 1) @ mel_fb [n_fft/2+1][n_mels]
+ * -> log(clamp(., 1e-7)) into out [B][n_mels][L/hop + 1].  Replaces torchaudio MelSpectrogram +
+ * safe_log (indextts/utils/feature_extractors.py:24-50, indextts/utils/common.py:110-121,
+ * infer.py:509-514).  n_fft a power of two <= 2048, L > n_fft/2. */
+int itts_log_mel(const float* audio, int64_t ld_audio, int B, int L, const float* window, const float* mel_fb,
+                 int n_fft, int hop, int n_mels, float* out, void* stream);
+
 /* ---- GPT (UnifiedVoice + HF GPT-2) ------------------------------------------------------------ */
 
 /* y[r] = LN2(LN1(x[row_idx ? row_idx[r] : r])) (LN2 optional; eps 1e-5).  ln_1 / ln_2 / ln_f and

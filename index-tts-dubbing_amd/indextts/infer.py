@@ -173,7 +173,7 @@ class IndexTTS:
     # ------------------------------------------------------------------ shared driver
     def _prompt(self, audio_prompt):
         if self.cache_cond_mel is None or self.cache_audio_prompt != audio_prompt:
-            cond_mel = prompt_mel(audio_prompt).to(self.device)
+            cond_mel = prompt_mel(audio_prompt, self.device)  # resample + log-mel on the GPU
             self.cache_audio_prompt = audio_prompt
             self.cache_cond_mel = cond_mel
             self.engine._prompt_cache.clear()  # conditioning / speaker embedding follow the mel cache

@@ -74,7 +74,7 @@ def resample(wav: torch.Tensor, orig_sr: int, new_sr: int) -> torch.Tensor:
     shape = wav.shape
     x = wav.reshape(-1, 1, shape[-1])
     x = F.pad(x, (width, width + o))
-    y = F.conv1d(x, k.to(wav.dtype), stride=o)  # [N, new, frames]
+    y = F.conv1d(x, k.to(wav.device, wav.dtype), stride=o)  # [N, new, frames]
     y = y.transpose(1, 2).reshape(x.shape[0], -1)
     target = math.ceil(n * shape[-1] / o)
     return y[..., :target].reshape(*shape[:-1], -1)
@@ -120,9 +120,34 @@ class MelSpectrogramFeatures:
         return torch.log(torch.clamp(mel, min=1e-7))
 
 
-def prompt_mel(path: str) -> torch.Tensor:
-    """The prompt-mel pipeline of ``infer()`` (``indextts/infer.py:509-514``) -> [1, 100, frames]."""
+def log_mel_hip(audio: torch.Tensor, feats: "MelSpectrogramFeatures" = None) -> torch.Tensor:
+    """``MelSpectrogramFeatures()(audio)`` (center padding) on the GPU: audio [B, L] f32 on a HIP
+    device -> [B, n_mels, L // hop + 1] via the fused itts_log_mel kernel (csrc/frontend.hip)."""
+    from .. import _hip
+    feats = feats or MelSpectrogramFeatures()
+    assert feats.padding == "center" and feats.win == feats.n_fft, "HIP log-mel implements the center/full-window form"
+    lib = _hip.load()
+    x = audio.reshape(-1, audio.shape[-1]).float().contiguous()
+    B, L = x.shape
+    dev = x.device
+    window = torch.hann_window(feats.win, periodic=True, dtype=torch.float32, device=dev)
+    fb = feats.fb.to(dev, torch.float32).contiguous()
+    out = torch.empty(B, fb.shape[1], L // feats.hop + 1, device=dev)
+    _hip.check(lib.itts_log_mel(x.data_ptr(), x.stride(0), B, L, window.data_ptr(), fb.data_ptr(), feats.n_fft,
+                                feats.hop, fb.shape[1], out.data_ptr(), _hip.stream_ptr(dev)), "itts_log_mel")
+    return out.reshape(*audio.shape[:-1], out.shape[-2], out.shape[-1])
+
+
+def prompt_mel(path: str, device=None) -> torch.Tensor:
+    """The prompt-mel pipeline of ``infer()`` (``indextts/infer.py:509-514``) -> [1, 100, frames].
+    ``device`` (a HIP device): resampling and the log-mel run there (the mel on the HIP kernel);
+    None: the CPU restatement (used by the tests as the from-spec reference)."""
     audio, sr = load_wav(path)
     audio = torch.mean(audio, dim=0, keepdim=True)
+    if device is not None and torch.device(device).type == "cuda":
+        audio = audio.to(device)
+        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
+            audio = resample(audio, sr, 24000)
+        return log_mel_hip(audio)
     audio = resample(audio, sr, 24000)
     return MelSpectrogramFeatures()(audio)

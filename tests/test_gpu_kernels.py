@@ -2,6 +2,7 @@
 
 Tolerance: bf16 GEMM operands (the reference uses the same bf16-rounded operands) with f32
 accumulation -> |err| <= 1e-2 * (|A| @ |W|^T) (+ bf16 output rounding for bf16 outputs)."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -194,3 +195,15 @@ def test_attn_prefill_matches_torch(mode):
         kk = x[:, D:2 * D].view(n, H, 64).transpose(0, 1)
         # cache rows of every non-padding position (left-pad keys are never attended, not stored)
         torch.testing.assert_close(kc[i, :, p:n].float().cpu(), kk[:, p:].to(cdt).float(), rtol=0, atol=0)
+
+
+def test_log_mel_kernel_matches_cpu_front_end():
+    """itts_log_mel (direct DFT per frame on the GPU) vs the CPU MelSpectrogramFeatures restatement."""
+    from indextts.utils.audio import MelSpectrogramFeatures, log_mel_hip
+    g = torch.Generator().manual_seed(0)
+    for L in (24000 // 3, 12345):
+        x = 0.3 * torch.randn(2, L, generator=g)
+        want = MelSpectrogramFeatures()(x)
+        got = log_mel_hip(x.cuda()).cpu()
+        assert got.shape == want.shape
+        np.testing.assert_allclose(got.exp().numpy(), want.exp().numpy(), rtol=2e-4, atol=2e-5)

@@ -57,3 +57,23 @@ def test_pack_layout():
     assert p.shape == (2, co, ci) and p.dtype == torch.bfloat16
     assert torch.equal(p[1, :40, :24].float(), w[1].to(torch.bfloat16).float())
     assert float(p[:, 40:].abs().sum()) == 0 and float(p[:, :, 24:].abs().sum()) == 0
+
+
+def test_mel_front_end_matches_numpy_restatement():
+    """MelSpectrogramFeatures (CPU restatement of torchaudio MelSpectrogram + safe_log; parity unpinned:
+    torchaudio is absent) vs a from-spec numpy version (reflect pad, periodic Hann, rfft, HTK mels)."""
+    import numpy as np
+    import torch
+    from indextts.utils.audio import MelSpectrogramFeatures, mel_filterbank
+    g = np.random.default_rng(0)
+    x = (0.3 * g.standard_normal(24000 // 2)).astype(np.float32)
+    got = MelSpectrogramFeatures()(torch.from_numpy(x)[None])[0].numpy()
+    n_fft, hop = 1024, 256
+    xp = np.pad(x.astype(np.float64), (n_fft // 2, n_fft // 2), mode="reflect")
+    win = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(n_fft) / n_fft)
+    frames = np.stack([xp[i * hop: i * hop + n_fft] * win for i in range(len(x) // hop + 1)])
+    mag = np.abs(np.fft.rfft(frames, axis=1))
+    fb = mel_filterbank(n_fft // 2 + 1, 0.0, 12000.0, 100, 24000).double().numpy()
+    want = np.log(np.maximum(mag @ fb, 1e-7)).T
+    assert got.shape == want.shape
+    np.testing.assert_allclose(np.exp(got), np.exp(want), rtol=1e-4, atol=1e-5)
