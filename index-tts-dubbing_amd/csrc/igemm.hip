@@ -12,7 +12,7 @@
 // Epilogue: v = acc + bias[n] + bias_b[b][n]; if gelu: v = gelu_tanh(v); v = alpha*(v + r1 + r2)
 // (r1/r2 residual tensors with Y's layout and dtype; r1 may alias Y).
 //
-// Tiling: 256 threads = 4 waves; block tile TM x TN, K step KC (channels of one tap) staged
+// Tiling: one wave per WM x WN sub-tile of the TM x TN block tile, K step KC (channels of one tap) staged
 // through double-buffered LDS (row pitch padded by 16 B -> conflict-free ds_read_b128 fragments),
 // with a 3-deep register ring (K-step it+2's global loads in flight while step it computes).
 // Tiles are remapped XCD-aware (output-channel tiles of one row tile run together on one XCD).
@@ -45,12 +45,13 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 }
 
 template <int TM, int TN, int WM, int WN, int KC, bool VEC, typename OutT>
-__global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
+__global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArgs p) {
+  constexpr int NT = 64 * (TM / WM) * (TN / WN);  // threads (one wave per WM x WN sub-tile)
   constexpr int PITCH = KC * 2 + 16;            // bytes per LDS row
   constexpr int A_BYTES = TM * PITCH, B_BYTES = TN * PITCH;
   constexpr int VPR = KC / 8;                   // 16-B vectors per row
   constexpr int A_TOT = TM * VPR, B_TOT = TN * VPR;  // 16-B vectors per tile
-  constexpr int A_VEC = (A_TOT + 255) / 256, B_VEC = (B_TOT + 255) / 256;
+  constexpr int A_VEC = (A_TOT + NT - 1) / NT, B_VEC = (B_TOT + NT - 1) / NT;
   constexpr int FM = WM / 32, FN = WN / 32;     // MFMA tiles per wave
   constexpr int WAVES_N = TN / WN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
     const int toff = p.tap_off[j];
 #pragma unroll
     for (int i = 0; i < A_VEC; ++i) {
-      const int v = tid + 256 * i, row = v / VPR, cv = (v % VPR) * 8;
+      const int v = tid + NT * i, row = v / VPR, cv = (v % VPR) * 8;
       const int t = q0 + row + toff, c = c0 + cv;
       u32x4_t val = {0u, 0u, 0u, 0u};
       if (v < A_TOT && t >= 0 && t < len) {
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
     const uint16_t* Wj = p.w + ((int64_t)j * p.co_pad + n0) * p.ci_pad + c0;
 #pragma unroll
     for (int i = 0; i < B_VEC; ++i) {
-      const int v = tid + 256 * i, row = v / VPR, cv = (v % VPR) * 8;
+      const int v = tid + NT * i, row = v / VPR, cv = (v % VPR) * 8;
       if (v < B_TOT) r.b[i] = *reinterpret_cast<const u32x4_t*>(Wj + (int64_t)row * p.ci_pad + cv);
     }
   };
@@ -112,12 +113,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgArgs p) {
     unsigned char* Bs = As + A_BYTES;
 #pragma unroll
     for (int i = 0; i < A_VEC; ++i) {
-      const int v = tid + 256 * i, row = v / VPR, cv = v % VPR;
+      const int v = tid + NT * i, row = v / VPR, cv = v % VPR;
       if (v < A_TOT) *reinterpret_cast<u32x4_t*>(As + row * PITCH + cv * 16) = r.a[i];
     }
 #pragma unroll
     for (int i = 0; i < B_VEC; ++i) {
-      const int v = tid + 256 * i, row = v / VPR, cv = v % VPR;
+      const int v = tid + NT * i, row = v / VPR, cv = v % VPR;
       if (v < B_TOT) *reinterpret_cast<u32x4_t*>(Bs + row * PITCH + cv * 16) = r.b[i];
     }
   };
@@ -202,16 +203,22 @@ template <int TM, int TN, int WM, int WN, int KC, typename OutT>
 void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
   dim3 grid(((a.Tmax + TM - 1) / TM) * ((a.Cout + TN - 1) / TN) * a.B);
   size_t lds = 2 * (size_t)(TM + TN) * (KC * 2 + 16);
+  constexpr int NT = 64 * (TM / WM) * (TN / WN);
   if (vec)
-    hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT>), grid, dim3(NT), lds, s, a);
   else
-    hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, false, OutT>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, false, OutT>), grid, dim3(NT), lds, s, a);
 }
 
 template <typename OutT>
 void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
   const bool wide_n = a.Cout >= 128, wide_k = a.Cin >= 128;
-  if (wide_n && wide_k) launch_cfg<128, 128, 64, 64, 64, OutT>(a, vec, s);
+  // wide layers: 8 waves per 128 x 128 tile (64 x 32 each) -- more waves per CU to hide the staging
+  // latency than 4 waves of 64 x 64 (+25-30 % on the latent-pass GEMMs, profiles/ubench_igemm.py);
+  // Cout = 192 (stage 2): 128 x 64 tiles of 8 x (32 x 32) instead of a half-empty second 128-column tile
+  if (wide_n && wide_k && a.Cout % 128 == 0) launch_cfg<128, 128, 64, 32, 64, OutT>(a, vec, s);
+  else if (wide_n && wide_k && a.Cout % 64 == 0) launch_cfg<128, 64, 32, 32, 64, OutT>(a, vec, s);
+  else if (wide_n && wide_k) launch_cfg<128, 128, 64, 64, 64, OutT>(a, vec, s);
   else if (wide_n) launch_cfg<128, 128, 64, 64, 32, OutT>(a, vec, s);
   else if (wide_k) launch_cfg<128, 32, 32, 32, 64, OutT>(a, vec, s);
   else launch_cfg<128, 32, 32, 32, 32, OutT>(a, vec, s);
