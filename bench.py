@@ -158,10 +158,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ITTS_BENCH_DEVICE / ITTS_DIST_BACKEND=gloo: rehearse the N-rank path with several ranks on one GPU
+    # (RCCL refuses two ranks on one device); the product setting is one rank per GPU over RCCL
+    local = int(os.environ.get("ITTS_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("ITTS_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from indextts.pipeline import BatchedTTS, SR
     from indextts.sharding import gather_waveforms, shard

@@ -25,6 +25,8 @@ def gather_waveforms(rows: List[torch.Tensor], n_total: int, device=None) -> Opt
     -> on rank 0 the ``n_total`` waveforms in utterance order; None on other ranks."""
     world, rank = dist.get_world_size(), dist.get_rank()
     device = torch.device(device) if device is not None else (rows[0].device if rows else torch.device("cpu"))
+    if dist.get_backend() == "gloo":  # gloo collectives run on host buffers
+        device = torch.device("cpu")
     per = (n_total + world - 1) // world  # max utterances per rank
     mine = shard(n_total, world, rank)
     assert len(rows) == len(mine), (len(rows), len(mine))
