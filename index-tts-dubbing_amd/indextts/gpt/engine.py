@@ -118,19 +118,34 @@ class HipGPT:
         conds = conds.to(self.dev).float()
         ncond = conds.shape[1]
         s = ncond + L + 2
-        emb = torch.zeros(B, s + 1, self.D, device=self.dev)
-        pads = []
-        for i in range(B):
-            row = text_ids[i].to(self.dev).long()
-            row = row[(row != self.stop_text) & (row != self.start_text)]
-            row = torch.cat([row.new_tensor([self.start_text]), row, row.new_tensor([self.stop_text])])
-            te = self.text_emb[row] + self.text_pos[: row.numel()]
-            c = conds[0] if conds.shape[0] == 1 else conds[i]
-            pad = L + 2 - row.numel()
-            emb[i, pad:s] = torch.cat([c, te], 0)
-            pads.append(pad)
+        D, dev = self.D, self.dev
+        # vectorised over rows (no host sync): kept ids packed to the right end of the [B, L+2] text
+        # block behind the start id, the stop id last; rows left-padded with zero embeddings
+        ids = text_ids.to(dev).long()
+        keep = (ids != self.stop_text) & (ids != self.start_text)
+        cnt = keep.sum(1)                                           # [B]
+        pad = L - cnt                                               # = L + 2 - (cnt + 2)
+        rank = torch.cumsum(keep.long(), 1) - 1                     # position among the kept ids
+        dst = pad[:, None] + 1 + rank                               # column in the [L+2] text block
+        tok = torch.full((B, L + 2), self.start_text, dtype=torch.long, device=dev)
+        tok.scatter_(1, torch.where(keep, dst, torch.full_like(dst, L + 1)), torch.where(keep, ids, torch.full_like(ids, self.stop_text)))
+        tok[torch.arange(B, device=dev), pad + cnt + 1] = self.stop_text
+        col = torch.arange(L + 2, device=dev)[None, :]
+        tpos = (col - pad[:, None]).clamp(min=0)                    # text positions restart at 0 per row
+        te = self.text_emb[tok] + self.text_pos[tpos]               # [B, L+2, D]
+        cb = conds.expand(B, -1, -1) if conds.shape[0] == 1 else conds
+        # the conditioning block sits right before the row's text: rows [pad, pad + ncond)
+        blk = torch.cat([cb, te], 1)                                # [B, ncond + L + 2, D] (unpadded order)
+        j = torch.arange(s, device=dev)[None, :]                    # output column
+        srcc = j - pad[:, None]                                     # source column (negative: padding)
+        valid = srcc >= 0
+        # the text block's padded prefix columns of `te` must be skipped: source index in blk
+        srcb = torch.where(srcc < ncond, srcc, ncond + pad[:, None] + (srcc - ncond))
+        g = torch.gather(blk, 1, srcb.clamp(min=0, max=ncond + L + 1)[..., None].expand(B, s, D))
+        emb = torch.zeros(B, s + 1, D, device=dev)
+        emb[:, :s] = g * valid[..., None]
         emb[:, s] = self.mel_emb[self.start_mel] + self.mel_pos[0]
-        return emb, torch.tensor(pads, dtype=torch.int32, device=self.dev), s
+        return emb, pad.int(), s
 
     # ---------------- GEMM dispatch ----------------
     def _gemm(self, A, w, Y, bias=None, gelu=False, residual=False):
@@ -660,33 +675,48 @@ class HipGPT:
         -> (latent [B, Tmax, D] in the vocoder's input layout (bf16 in bf16 mode), lengths [B])."""
         B = len(text_list)
         conds = conds.to(self.dev).float()
-        rows, starts, lens, mel_rows = [], [], [], []
-        M = 0
+        ncond, D, dev = conds.shape[1], self.D, self.dev
+        # all index arithmetic on the host (one copy of the text ids down, one of each index up), then
+        # three gathers build the packed [M, D] input: [conds ; text_emb + text_pos ; mel_emb + mel_pos]
+        t_host = [t.reshape(-1) for t in text_list]
+        t_all = torch.cat([t.to(dev) for t in t_host]).long().cpu().numpy() if B else np.zeros(0, np.int64)
+        lt = np.array([t.numel() for t in t_host], dtype=np.int64)
+        codes_np = [np.asarray(c.reshape(-1).cpu(), dtype=np.int64) for c in codes_list]
+        n = [int(c.shape[0]) for c in codes_np]
+        lens = (ncond + lt + 2 + np.array(n, dtype=np.int64) + 2).tolist()
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        M = int(sum(lens))
+        cond_dst, cond_src, txt_dst, txt_tok, txt_pos, mel_dst, mel_tok, mel_pos = ([] for _ in range(8))
+        toff = np.concatenate([[0], np.cumsum(lt)[:-1]]).astype(np.int64)
         for b in range(B):
-            t = text_list[b].to(self.dev).long().reshape(-1)
-            c = codes_list[b].to(self.dev).long().reshape(-1)
-            t = torch.cat([t.new_tensor([self.start_text]), t, t.new_tensor([self.stop_text])])
-            m = torch.cat([c.new_tensor([self.start_mel]), c, c.new_tensor([self.stop_mel])])
-            cb = conds[0] if conds.shape[0] == 1 else conds[b]
-            x = torch.cat([cb, self.text_emb[t] + self.text_pos[: t.numel()],
-                           self.mel_emb[m] + self.mel_pos[: m.numel()]], 0)
-            rows.append(x)
-            starts.append(M)
-            lens.append(x.shape[0])
-            first = M + cb.shape[0] + t.numel()
-            mel_rows.append(torch.arange(first, first + c.numel(), device=self.dev))
-            M += x.shape[0]
-        x = torch.cat(rows, 0).contiguous()
-        s_t = torch.tensor(starts, dtype=torch.int32, device=self.dev)
-        l_t = torch.tensor(lens, dtype=torch.int32, device=self.dev)
+            s0 = int(starts[b])
+            cond_dst.append(np.arange(s0, s0 + ncond))
+            cond_src.append((0 if conds.shape[0] == 1 else b) * ncond + np.arange(ncond))
+            tt = np.concatenate([[self.start_text], t_all[toff[b]: toff[b] + lt[b]], [self.stop_text]])
+            txt_dst.append(s0 + ncond + np.arange(tt.shape[0]))
+            txt_tok.append(tt)
+            txt_pos.append(np.arange(tt.shape[0]))
+            mm = np.concatenate([[self.start_mel], codes_np[b], [self.stop_mel]])
+            m0 = s0 + ncond + tt.shape[0]
+            mel_dst.append(m0 + np.arange(mm.shape[0]))
+            mel_tok.append(mm)
+            mel_pos.append(np.arange(mm.shape[0]))
+        up = lambda parts: torch.from_numpy(np.concatenate(parts).astype(np.int64)).to(dev)  # noqa: E731
+        x = torch.empty(M, D, device=dev)
+        x[up(cond_dst)] = conds.reshape(-1, D)[up(cond_src)]
+        x[up(txt_dst)] = self.text_emb[up(txt_tok)] + self.text_pos[up(txt_pos)]
+        x[up(mel_dst)] = self.mel_emb[up(mel_tok)] + self.mel_pos[up(mel_pos)]
+        s_t = torch.from_numpy(starts.astype(np.int32)).to(dev)
+        l_t = torch.tensor(lens, dtype=torch.int32, device=dev)
         self._forward_rows(x, s_t, l_t, None, max(lens))
-        n = [int(c.numel()) for c in codes_list]
         Tmax = max(n)
-        idx = torch.zeros(B, Tmax, dtype=torch.int32, device=self.dev)
-        for b in range(B):
-            idx[b, : n[b]] = mel_rows[b].int()
+        idx = np.zeros((B, Tmax), dtype=np.int32)
+        for b in range(B):  # latent rows: the first n of the mel block (start token .. code n-2), :-2 of
+            first = int(starts[b]) + ncond + int(lt[b]) + 2  # gpt/model.py:575-578
+            idx[b, : n[b]] = np.arange(first, first + n[b])
         out = torch.empty(B, Tmax, self.D, dtype=self.act_dtype, device=self.dev)
-        self._ln(x, out.view(B * Tmax, self.D), self.ln_f, self.final_norm, idx=idx.view(-1), M=B * Tmax)
+        self._ln(x, out.view(B * Tmax, self.D), self.ln_f, self.final_norm,
+                 idx=torch.from_numpy(idx).to(dev).view(-1), M=B * Tmax)
         return out, torch.tensor(n, dtype=torch.int32)
 
 
