@@ -18,7 +18,10 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTO = 16;   // outputs per thread along time
+#ifndef ITTS_ACT_TO
+#define ITTS_ACT_TO 16
+#endif
+constexpr int kTO = ITTS_ACT_TO;  // outputs per thread along time
 constexpr int kHalo = 6;  // input samples each side that one output depends on
 
 struct ActArgs {
@@ -33,9 +36,11 @@ struct ActArgs {
   int64_t sxb, sxt, sxc, syb, syt, syc;
 };
 
-__device__ __forceinline__ float snake(float u, float a, float inv_b) {
-  float s = __sinf(u * a);  // v_sin_f32 (range-reduced in revolutions); accurate sinf was ~2x the kernel time
-  return u + inv_b * (s * s);
+// a_rev = exp(alpha) / (2 pi): v_sin_f32 takes revolutions, so sin(u * a) is one multiply + v_sin
+// (__sinf would add a second multiply by 1/(2 pi)); accurate sinf was ~2x the kernel time
+__device__ __forceinline__ float snake(float u, float a_rev, float inv_b) {
+  const float s = __builtin_amdgcn_sinf(u * a_rev);
+  return fmaf(inv_b, s * s, u);
 }
 
 template <typename TI, typename TO, bool VEC>
@@ -54,7 +59,7 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
   if constexpr (VEC) {
     // channel-last bf16 with C % 8 == 0: 16-B loads, every load of the tile issued before the
     // first LDS write (one memory latency per block instead of one per loop trip)
-    constexpr int kMaxV = 3;  // vectors per thread: rows*CT/8 = (256/CT*16 + 12)*CT/8 <= 608 for CT <= 64
+    constexpr int kMaxV = kTO <= 16 ? 3 : 5;  // vectors per thread: rows*CT/8 = (256/CT*kTO + 12)*CT/8
     const int cv = CT / 8, nv = rows * cv;
     u32x4_t buf[kMaxV];
 #pragma unroll
@@ -73,12 +78,12 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
       const int v = threadIdx.x + kThreads * i;
       if (v < nv) {
         const int r = v / cv, c = (v - r * cv) * 8;
-        float* d = xs + r * CT + c;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          d[2 * e] = __uint_as_float(buf[i][e] << 16);
-          d[2 * e + 1] = __uint_as_float(buf[i][e] & 0xFFFF0000u);
-        }
+        // two 16-B LDS writes per vector (eight 4-B writes 32 B apart were 8-way bank conflicts)
+        f32x4_t* d = reinterpret_cast<f32x4_t*>(xs + r * CT + c);
+        d[0] = f32x4_t{__uint_as_float(buf[i][0] << 16), __uint_as_float(buf[i][0] & 0xFFFF0000u),
+                       __uint_as_float(buf[i][1] << 16), __uint_as_float(buf[i][1] & 0xFFFF0000u)};
+        d[1] = f32x4_t{__uint_as_float(buf[i][2] << 16), __uint_as_float(buf[i][2] & 0xFFFF0000u),
+                       __uint_as_float(buf[i][3] << 16), __uint_as_float(buf[i][3] & 0xFFFF0000u)};
       }
     }
   } else {
@@ -98,8 +103,8 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
   if (ts >= len) return;
   float f[12], g[12];
 #pragma unroll
-  for (int k = 0; k < 12; ++k) { f[k] = p.up[k]; g[k] = p.down[k]; }
-  const float a = expf(p.log_alpha[ch]);
+  for (int k = 0; k < 12; ++k) { f[k] = 2.0f * p.up[k]; g[k] = p.down[k]; }  // x2: the up-sampler gain (exact)
+  const float a = expf(p.log_alpha[ch]) * 0.15915494309189535f;
   const float inv_b = 1.0f / (expf(p.log_beta[ch]) + 1e-9f);
   const float* col = xs + (sub * kTO) * CT + c;  // row r <-> t = ts - 6 + r
 
@@ -118,7 +123,7 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
 #pragma unroll
         for (int q = -2; q <= 3; ++q) acc = fmaf(xr[3 + j / 2 + q], f[6 - 2 * q], acc);
       }
-      v[j] = snake(2.0f * acc, a, inv_b);
+      v[j] = snake(acc, a, inv_b);
     }
 #pragma unroll
     for (int i = 0; i < kTO; ++i) {
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
         } else {
           for (int q = -2; q <= 3; ++q) acc = fmaf(col[(min(max(pp + q, 0), len - 1) - base) * CT], f[6 - 2 * q], acc);
         }
-        o = fmaf(g[k], snake(2.0f * acc, a, inv_b), o);
+        o = fmaf(g[k], snake(acc, a, inv_b), o);
       }
       St<TO>::st(y + (int64_t)t * p.syt + (int64_t)ch * p.syc, o);
     }

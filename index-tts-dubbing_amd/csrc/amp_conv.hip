@@ -51,9 +51,10 @@ struct AcArgs {
   int tap_off[kMaxTapsAc];
 };
 
-__device__ __forceinline__ float snake_f(float u, float a, float inv_b) {
-  const float s = __sinf(u * a);
-  return u + inv_b * (s * s);
+// a_rev = exp(alpha) / (2 pi): v_sin_f32 takes revolutions (see act.hip)
+__device__ __forceinline__ float snake_f(float u, float a_rev, float inv_b) {
+  const float s = __builtin_amdgcn_sinf(u * a_rev);
+  return fmaf(inv_b, s * s, u);
 }
 
 __device__ __forceinline__ float ld_bf(const uint16_t* p) { return __uint_as_float(((uint32_t)*p) << 16); }
@@ -137,12 +138,12 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
     const int nstrip = (WR + SR - 1) / SR;
     float f[12], g[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) { f[k] = p.up[k]; g[k] = p.down[k]; }
+    for (int k = 0; k < 12; ++k) { f[k] = 2.0f * p.up[k]; g[k] = p.down[k]; }  // x2: up-sampler gain (exact)
     for (int item = tid; item < nstrip * Cin; item += 256) {
       const int s = item / Cin, c = item - s * Cin;
       const int r0 = s * SR;
       uint16_t* dst = reinterpret_cast<uint16_t*>(Aw) + c;  // row pitch PA/2 elements
-      const float a = expf(p.log_alpha[c]);
+      const float a = expf(p.log_alpha[c]) * 0.15915494309189535f;
       const float inv_b = 1.0f / (expf(p.log_beta[c]) + 1e-9f);
       const int t0 = q0 - p.hl + r0;  // time of row r0; raw rows r0 .. r0+SR+11 hold x[t0-6 ..]
       const uint16_t* col = xr + r0 * Cin + c;
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
 #pragma unroll
             for (int q = -2; q <= 3; ++q) acc = fmaf(xv[3 + j / 2 + q], f[6 - 2 * q], acc);
           }
-          v[j] = snake_f(2.0f * acc, a, inv_b);
+          v[j] = snake_f(acc, a, inv_b);
         }
 #pragma unroll
         for (int i = 0; i < SR; ++i) {
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
               for (int q = -3; q <= 2; ++q) ae = fmaf(ld_bf(xp + q * Cin), f[5 - 2 * q], ae);
 #pragma unroll
               for (int q = -2; q <= 3; ++q) ao = fmaf(ld_bf(xp + q * Cin), f[6 - 2 * q], ao);
-              o = fmaf(g[k], snake_f(2.0f * ((m & 1) ? ao : ae), a, inv_b), o);
+              o = fmaf(g[k], snake_f((m & 1) ? ao : ae, a, inv_b), o);
             }
           }
           dst[(r0 + i) * (PA / 2)] = f2bf(o);  // rows outside [0, len): the conv's zero padding
