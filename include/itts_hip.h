@@ -114,6 +114,13 @@ int itts_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, int 
 int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed, int K, int N, int M, const float* bias,
                      const float* g1, const float* b1, const float* g2, const float* b2, int lnmode, int gelu, int epi,
                      void* y, int64_t ldy, int out_dtype, int64_t split_stride, int ksplit, void* stream);
+/* The same store-epilogue GEMM on 16-column tiles (v_mfma_f32_16x16x32_bf16): y = act(a @ W^T + bias)
+ * as out_dtype, act = gelu_tanh when gelu; weights prepacked [N/16][K/32][64][8] bf16 (lane 16q + c
+ * holds W^T[16nt + c][32s + 8q : +8]); a bf16 with rows padded to whole 32-row tiles.  c_fc + gelu and
+ * mel_head of the KV-cached decode (HF modeling_gpt2.py:229-243; gpt/model.py:180): twice the
+ * workgroups of itts_decode_gemm, half the weight bytes each. */
+int itts_decode_gemm16(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M, const float* bias,
+                       int gelu, void* y, int64_t ldy, int out_dtype, void* stream);
 /* One decode step of 16x64 causal attention per row: appends this step's k/v at position
  * kv_base + tstate[0] of the cache [B][H][smax][64] and attends over the valid (pad-masked,
  * quirk Q2) prefix.  HF modeling_gpt2.py:54-72,185-225 with the additive padding mask. */
@@ -131,6 +138,16 @@ int itts_attn_decode_rows(const float* qkv, int64_t ldqkv, int nsplit, int64_t s
                           const int32_t* pad, int kv_base, const int32_t* tstate, void* out, int64_t ldo, int B,
                           int H, int cache_dtype, int out_dtype, const int32_t* kv_rows, int64_t ld_rows,
                           void* stream);
+/* Attention with attn.c_proj fused (bf16 product decode; kv_rows nullable, as itts_attn_decode_rows):
+ * per (row b, head h) the f32 head output o_h [64] times rows 64h .. 64h+63 of w_proj (the c_proj
+ * weight in HF Conv1D [in = H*64][out = N] order, bf16) is written as the split-K partial
+ * part[h*part_stride + b*ldp + n], n < N (N % 8 == 0, N <= 1024); itts_residual_reduce_ln with
+ * nsplit = H sums the heads with the bias and the residual.  HF modeling_gpt2.py:185-225. */
+int itts_attn_decode_proj(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride, const float* qkv_bias,
+                          void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs, int smax,
+                          const int32_t* pad, int kv_base, const int32_t* tstate, const void* w_proj, int N,
+                          float* part, int64_t part_stride, int64_t ldp, int B, int H, int cache_dtype,
+                          const int32_t* kv_rows, int64_t ld_rows, void* stream);
 /* Causal attention over packed variable-length sequences (prefill and latent pass); optionally
  * writes K/V into the decode cache.  seq_pad[b] leading rows are masked (left padding, Q2). */
 int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start, const int32_t* seq_len,

@@ -55,20 +55,35 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 #ifndef ITTS_ATTN_WPS
 #define ITTS_ATTN_WPS 1
 #endif
-template <typename TC, typename TO, int NT, bool ROWS>
-__global__ __launch_bounds__(NT, ITTS_ATTN_WPS) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
+#ifndef ITTS_ATTN_PROJ_WPS  // fused c_proj: 256 VGPRs without spills at 1; 2 spills 96 VGPRs
+#define ITTS_ATTN_PROJ_WPS 1
+#endif
+// PROJ (attn.c_proj fused, bf16 product decode): the head's output o_h [64] (f32, never rounded)
+// times its 64 rows of the c_proj weight W [H*64][N] (HF Conv1D [in, out] order, bf16) is written as
+// the split-K partial part[h][b][0..N) (split = head); itts_residual_reduce_ln sums the H partials
+// with the bias and the residual.  W's rows do not depend on this step either: they are requested
+// right after the q/k/v slab loads (thread (kh, j) holds rows 64h + 32kh .. +31, columns 8j .. 8j+7)
+// and arrive while the keys stream.  The 32 workgroups of one head land on one XCD (dispatch is
+// round-robin over XCDs and the grid is head-fastest), so each XCD's L2 holds only 2 heads' rows.
+// One kernel boundary and the separate c_proj launch less per layer.
+template <typename TC, typename TO, int NT, bool ROWS, bool PROJ>
+__global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
                                                          int64_t split_stride, const float* __restrict__ qkv_bias,
                                                          TC* __restrict__ cache_k, TC* __restrict__ cache_v,
                                                          int64_t cache_bs, int64_t cache_hs, const int32_t* pad,
                                                          int kv_base, const int32_t* __restrict__ tstate,
                                                          TO* __restrict__ out, int64_t ldo, int H,
-                                                         const int32_t* __restrict__ kv_rows, int64_t ld_rows) {
+                                                         const int32_t* __restrict__ kv_rows, int64_t ld_rows,
+                                                         const uint16_t* __restrict__ wproj, int N,
+                                                         float* __restrict__ part, int64_t part_stride, int64_t ldp) {
+  static_assert(!PROJ || NT == 256, "the c_proj epilogue maps 256 threads onto 2 x 128 column slots");
   constexpr int NG = NT / 8;
   constexpr int KB = ITTS_ATTN_KB;               // keys per group per round (packed rows in registers)
   constexpr int RW = sizeof(TC) * 8 / 16;       // 16-B vectors per lane per row (bf16: 1, f32: 2)
   __shared__ float qs[kHD], kn[kHD], vn[kHD];
   __shared__ float gm[NG], gl[NG];
   __shared__ float pv[NG][kHD + 1];
+  __shared__ float ofin[PROJ ? kHD : 1];  // PROJ: the merged head output
   const int h = blockIdx.x, b = blockIdx.y;
   const int D = H * kHD;
   const int kidx = kv_base + tstate[0];
@@ -118,6 +133,18 @@ __global__ __launch_bounds__(NT, ITTS_ATTN_WPS) void attn_decode_kernel(const fl
     } else {
       vn[d] = v;
       St<TC>::st(Vc + (int64_t)kidx * kHD + d, v);
+    }
+  }
+  // (2b) PROJ: this head's 64 rows of W, issued after the slab loads so that the wait for the slabs
+  // above does not include them (loads retire in order)
+  constexpr int PK = PROJ ? kHD / 2 : 1;
+  const int kh = threadIdx.x >> 7, pj = threadIdx.x & 127, n0 = 8 * pj;
+  u32x4_t wr[PK];
+  if constexpr (PROJ) {
+    if (n0 < N) {
+      const uint16_t* wsrc = wproj + (int64_t)(h * kHD + kh * PK) * N + n0;
+#pragma unroll
+      for (int k = 0; k < PK; ++k) wr[k] = *reinterpret_cast<const u32x4_t*>(wsrc + (int64_t)k * N);
     }
   }
   __syncthreads();
@@ -215,7 +242,38 @@ __global__ __launch_bounds__(NT, ITTS_ATTN_WPS) void attn_decode_kernel(const fl
       L = fmaf(gl[i], w, L);
       acc = fmaf(pv[i][threadIdx.x], w, acc);
     }
-    St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, acc / L);
+    if constexpr (PROJ) ofin[threadIdx.x] = acc / L;
+    else St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, acc / L);
+  }
+  if constexpr (PROJ) {
+    // (4) part[h][b][n] = sum_d o_h[d] * W[64h + d][n]: each half of the workgroup sums 32 rows of W,
+    // the halves combine through LDS in a fixed order (rows 0..31, then 32..63)
+    __syncthreads();
+    float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (n0 < N) {
+#pragma unroll
+      for (int k = 0; k < PK; ++k) {
+        const float ov = ofin[kh * PK + k];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a8[2 * i] = fmaf(ov, __uint_as_float(wr[k][i] << 16), a8[2 * i]);
+          a8[2 * i + 1] = fmaf(ov, __uint_as_float(wr[k][i] & 0xFFFF0000u), a8[2 * i + 1]);
+        }
+      }
+    }
+    float* xch = &pv[0][0];  // [8][128]: pv's last readers (the merge) are past the barrier above
+    if (kh == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xch[e * 128 + pj] = a8[e];
+    }
+    __syncthreads();
+    if (kh == 0 && n0 < N) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a8[e] += xch[e * 128 + pj];
+      f32x4_t* dst = reinterpret_cast<f32x4_t*>(part + (int64_t)h * part_stride + (int64_t)b * ldp + n0);
+      dst[0] = f32x4_t{a8[0], a8[1], a8[2], a8[3]};
+      dst[1] = f32x4_t{a8[4], a8[5], a8[6], a8[7]};
+    }
   }
 }
 
@@ -467,28 +525,41 @@ int attn_decode_launch(const char* fn, const float* qkv, int64_t ldqkv, int nspl
                        const float* qkv_bias, void* cache_k, void* cache_v, int64_t cache_bs, int64_t cache_hs,
                        int smax, const int32_t* pad, int kv_base, const int32_t* tstate, void* out, int64_t ldo,
                        int B, int H, int cache_dtype, int out_dtype, const int32_t* kv_rows, int64_t ld_rows,
-                       void* stream) {
+                       const void* wproj, int N, float* part, int64_t part_stride, int64_t ldp, void* stream) {
   ITTS_REQUIRE(B >= 0 && H > 0 && nsplit >= 1, fn, "bad sizes");
   if (B == 0) return 0;
-  ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && out, fn, "null pointer");
+  ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && (out || wproj), fn, "null pointer");
   ITTS_REQUIRE(smax <= kMaxKeys && cache_hs >= (int64_t)smax * kHD, fn, "bad cache capacity");
+  ITTS_REQUIRE(!wproj || (part && N > 0 && N <= 1024 && N % 8 == 0 && ldp >= N && ldp % 4 == 0 &&
+                          part_stride % 4 == 0 &&
+                          ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(wproj)) & 15) == 0),
+               fn, "c_proj partials need N % 8 == 0, N <= 1024 and 16-B aligned rows");
   dim3 grid(H, B);
   hipStream_t s = itts::as_stream(stream);
-#define ITTS_AD(TC, TO)                                                                                             \
+  const uint16_t* wp = static_cast<const uint16_t*>(wproj);
+#define ITTS_AD(TC, TO, PR)                                                                                         \
   do {                                                                                                            \
     if (kv_rows)                                                                                                  \
-      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, true>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,       \
+      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, true, PR>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,   \
                          split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base,      \
-                         tstate, (TO*)out, ldo, H, kv_rows, ld_rows);                                               \
+                         tstate, (TO*)out, ldo, H, kv_rows, ld_rows, wp, N, part, part_stride, ldp);                \
     else                                                                                                          \
-      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, false>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,      \
+      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, false, PR>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,  \
                          split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base,      \
-                         tstate, (TO*)out, ldo, H, nullptr, 0);                                                     \
+                         tstate, (TO*)out, ldo, H, nullptr, 0, wp, N, part, part_stride, ldp);                      \
   } while (0)
-  if (cache_dtype == ITTS_BF16 && out_dtype == ITTS_BF16) ITTS_AD(uint16_t, uint16_t);
-  else if (cache_dtype == ITTS_F32 && out_dtype == ITTS_F32) ITTS_AD(float, float);
-  else if (cache_dtype == ITTS_BF16) ITTS_AD(uint16_t, float);
-  else ITTS_AD(float, uint16_t);
+  if (wproj) {
+    if (cache_dtype == ITTS_BF16) ITTS_AD(uint16_t, float, true);
+    else ITTS_AD(float, float, true);
+  } else if (cache_dtype == ITTS_BF16 && out_dtype == ITTS_BF16) {
+    ITTS_AD(uint16_t, uint16_t, false);
+  } else if (cache_dtype == ITTS_F32 && out_dtype == ITTS_F32) {
+    ITTS_AD(float, float, false);
+  } else if (cache_dtype == ITTS_BF16) {
+    ITTS_AD(uint16_t, float, false);
+  } else {
+    ITTS_AD(float, uint16_t, false);
+  }
 #undef ITTS_AD
   return itts::check_launch(fn);
 }
@@ -500,7 +571,21 @@ extern "C" int itts_attn_decode(const float* qkv, int64_t ldqkv, int nsplit, int
                                 void* out, int64_t ldo, int B, int H, int cache_dtype, int out_dtype, void* stream) {
   return attn_decode_launch("itts_attn_decode", qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v,
                             cache_bs, cache_hs, smax, pad, kv_base, tstate, out, ldo, B, H, cache_dtype, out_dtype,
-                            nullptr, 0, stream);
+                            nullptr, 0, nullptr, 0, nullptr, 0, 0, stream);
+}
+
+extern "C" int itts_attn_decode_proj(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
+                                     const float* qkv_bias, void* cache_k, void* cache_v, int64_t cache_bs,
+                                     int64_t cache_hs, int smax, const int32_t* pad, int kv_base,
+                                     const int32_t* tstate, const void* w_proj, int N, float* part,
+                                     int64_t part_stride, int64_t ldp, int B, int H, int cache_dtype,
+                                     const int32_t* kv_rows, int64_t ld_rows, void* stream) {
+  const char* fn = "itts_attn_decode_proj";
+  ITTS_REQUIRE(w_proj, fn, "w_proj required");
+  ITTS_REQUIRE(!kv_rows || ld_rows >= smax, fn, "kv_rows [B][ld_rows >= smax] required");
+  return attn_decode_launch(fn, qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v, cache_bs, cache_hs,
+                            smax, pad, kv_base, tstate, nullptr, 0, B, H, cache_dtype, ITTS_F32, kv_rows, ld_rows,
+                            w_proj, N, part, part_stride, ldp, stream);
 }
 
 extern "C" int itts_attn_decode_rows(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,
@@ -512,7 +597,7 @@ extern "C" int itts_attn_decode_rows(const float* qkv, int64_t ldqkv, int nsplit
   ITTS_REQUIRE(kv_rows && ld_rows >= smax, fn, "kv_rows [B][ld_rows >= smax] required");
   return attn_decode_launch(fn, qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v, cache_bs, cache_hs,
                             smax, pad, kv_base, tstate, out, ldo, B, H, cache_dtype, out_dtype, kv_rows, ld_rows,
-                            stream);
+                            nullptr, 0, nullptr, 0, 0, stream);
 }
 
 extern "C" int itts_attn_prefill(const float* qkv, int64_t ldqkv, const int32_t* seq_start, const int32_t* seq_len,

@@ -217,6 +217,89 @@ void launch_dg(const DgArgs& a, int row_tiles, int ksplit, hipStream_t s) {
   }
 }
 
+// ---- 16-column tiles (v_mfma_f32_16x16x32_bf16) for the wide store-epilogue projections ----------
+// On 32-column tiles c_fc (N = 4096) and mel_head (N = 8194) launch 128 / 257 workgroups that stream
+// 64 KiB of weights each, and these latency-bound launches take about as long as one workgroup's
+// stream; on 16-column tiles they launch 256 / 513 workgroups of 32 KiB (every CU busy, half the
+// bytes per workgroup).  Weights [N/16][K/32][64 lanes][8] bf16: lane l = 16q + c holds
+// W^T[16nt + c][32s + 8q : +8] (pack_skinny16); one wave load = one contiguous 1 KiB.  A = bf16
+// [32-row tile][lda]; the two 16-row halves of the tile share every weight fragment.  Same wave /
+// k-step interleave, register pipeline and fixed-order cross-wave LDS reduction as decode_gemm_kernel
+// (bitwise batch-invariant per row).  Store epilogue only: y = act(acc + bias).
+template <int NW, typename OutT>
+__global__ __launch_bounds__(64 * NW) void decode_gemm16_kernel(DgArgs p) {
+  __shared__ float red[NW][8][64];
+  const int nt = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ksteps = p.K / 32;
+  const int niter = (ksteps - w + NW - 1) / NW;  // this wave's k-steps: w + NW*i
+  const u32x4_t* Wt = p.w + (int64_t)nt * ksteps * 64 + lane;
+  const int c16 = lane & 15, q = lane >> 4;
+  const uint16_t* A = reinterpret_cast<const uint16_t*>(p.a);
+
+  u32x4_t wa[kU] = {}, wb[kU] = {};  // zero-initialised: see decode_gemm_kernel
+  auto wload = [&](u32x4_t (&dst)[kU], int i0) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u < niter) dst[u] = __builtin_nontemporal_load(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
+  };
+  wload(wa, 0);
+  f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const u32x4_t (&src)[kU], int i0) {
+    bf16x8_t a0[kU] = {}, a1[kU] = {};
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u < niter) {
+        const int64_t col = 32 * (w + NW * (i0 + u)) + 8 * q;
+        a0[u] = *reinterpret_cast<const bf16x8_t*>(A + (int64_t)c16 * p.lda + col);
+        a1[u] = *reinterpret_cast<const bf16x8_t*>(A + (int64_t)(16 + c16) * p.lda + col);
+      }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u < niter) {
+        const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&src[u]);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bfr, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bfr, acc1, 0, 0, 0);
+      }
+  };
+  for (int i0 = 0; i0 < niter; i0 += 2 * kU) {
+    if (i0 + kU < niter) wload(wb, i0 + kU);
+    compute(wa, i0);
+    if (i0 + 2 * kU < niter) wload(wa, i0 + 2 * kU);
+    if (i0 + kU < niter) compute(wb, i0 + kU);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[w][r][lane] = acc0[r];
+    red[w][4 + r][lane] = acc1[r];
+  }
+  __syncthreads();
+  // 512 outputs (32 rows x 16 columns); C/D layout of 16x16x32: row = 4*(lane>>4) + reg, col = lane&15
+  for (int o = threadIdx.x; o < 512; o += 64 * NW) {
+    const int e = o >> 6, l = o & 63;  // e = 4 * (row half) + reg
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v += red[ww][e][l];
+    const int row = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
+    const int n = nt * 16 + (l & 15);
+    if (row >= p.M || n >= p.N) continue;
+    if (p.bias) v += p.bias[n];
+    if (p.gelu) v = gelu_tanh_d(v);
+    St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
+  }
+}
+
+template <int NW, typename OutT>
+void launch_dg16(const DgArgs& a, int row_tiles, hipStream_t s) {
+  for (int t = 0; t < row_tiles; ++t) {
+    DgArgs b = a;
+    b.M = a.M - 32 * t < 32 ? a.M - 32 * t : 32;
+    b.a = reinterpret_cast<const uint16_t*>(a.a) + (int64_t)t * 32 * a.lda;
+    b.y = reinterpret_cast<OutT*>(a.y) + (int64_t)t * 32 * a.ldy;
+    hipLaunchKernelGGL((decode_gemm16_kernel<NW, OutT>), dim3((a.N + 15) / 16), dim3(64 * NW), 0, s, b);
+  }
+}
+
 }  // namespace
 
 // lnmode: 0 = A is bf16; 1 = A = LN(X f32) with (g1,b1); 2 = A = LN(LN(X)) with (g1,b1) then (g2,b2).
@@ -268,5 +351,23 @@ extern "C" int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed
     else DG_LN(8, 2, 0, float);
   }
 #undef DG_LN
+  return itts::check_launch(fn);
+}
+
+// 16-column tiles, store epilogue: y = act(a @ W^T + bias) as out_dtype (act = gelu_tanh if gelu);
+// weights from pack_skinny16; a: bf16 rows padded to whole 32-row tiles.
+extern "C" int itts_decode_gemm16(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M,
+                                  const float* bias, int gelu, void* y, int64_t ldy, int out_dtype, void* stream) {
+  const char* fn = "itts_decode_gemm16";
+  ITTS_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 32 == 0, fn, "bad sizes (K must be a multiple of 32)");
+  if (M == 0) return 0;
+  ITTS_REQUIRE(a && w_packed16 && y, fn, "null pointer");
+  ITTS_REQUIRE(lda % 8 == 0 && (reinterpret_cast<uintptr_t>(a) & 15) == 0, fn, "A rows must be 16-B aligned");
+  DgArgs d{a, lda, static_cast<const u32x4_t*>(w_packed16), K, N, M, bias, nullptr, nullptr, nullptr, nullptr,
+           gelu, y, ldy, 0};
+  const int tiles = (M + 31) / 32;
+  hipStream_t s = itts::as_stream(stream);
+  if (out_dtype == ITTS_BF16) launch_dg16<8, uint16_t>(d, tiles, s);
+  else launch_dg16<8, float>(d, tiles, s);
   return itts::check_launch(fn);
 }

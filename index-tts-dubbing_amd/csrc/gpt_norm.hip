@@ -73,7 +73,7 @@ __global__ __launch_bounds__(kT) void ln_rows_kernel(const float* __restrict__ x
 // Decode-step variant: blockDim = D/4 threads, 4 consecutive elements (one float4) per thread, and
 // every load of the row (x, bias, all split partials) issued before the first use, so the kernel
 // pays one memory round trip instead of one per element group.
-constexpr int kMaxSplit = 8;
+constexpr int kMaxSplit = 16;  // 16: one partial per head from itts_attn_decode_proj
 
 __device__ __forceinline__ float block_sum_n(float v, float* red) {
   v = wave_sum(v);
@@ -86,14 +86,15 @@ __device__ __forceinline__ float block_sum_n(float v, float* red) {
   return s;
 }
 
-__device__ __forceinline__ void ln4(float (&v)[4], int D, const float* g, const float* b, float* red) {
+// g4 / b4: this thread's LayerNorm weights, loaded by the caller together with the row (they do not
+// depend on it, so their latency hides under the partial-sum loads instead of following the two
+// block reductions: a global load cannot move across the barriers)
+__device__ __forceinline__ void ln4(float (&v)[4], int D, const f32x4_t& g4, const f32x4_t& b4, float* red) {
   const float mean = block_sum_n(v[0] + v[1] + v[2] + v[3], red) / D;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) q += (v[i] - mean) * (v[i] - mean);
   const float rstd = rsqrtf(block_sum_n(q, red) / D + 1e-5f);
-  const f32x4_t g4 = *reinterpret_cast<const f32x4_t*>(g + 4 * threadIdx.x);
-  const f32x4_t b4 = *reinterpret_cast<const f32x4_t*>(b + 4 * threadIdx.x);
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = (v[i] - mean) * rstd * g4[i] + b4[i];
 }
@@ -112,6 +113,15 @@ __global__ __launch_bounds__(1024) void residual_reduce_ln_v4_kernel(
 #pragma unroll
   for (int s = 0; s < kMaxSplit; ++s)
     if (s < nsplit) pv[s] = *reinterpret_cast<const f32x4_t*>(part + s * split_stride + (int64_t)m * ldp + e);
+  f32x4_t g1v = {0.f, 0.f, 0.f, 0.f}, b1v = g1v, g2v = g1v, b2v = g1v;
+  if (g1) {
+    g1v = *reinterpret_cast<const f32x4_t*>(g1 + e);
+    b1v = *reinterpret_cast<const f32x4_t*>(b1 + e);
+  }
+  if (g2) {
+    g2v = *reinterpret_cast<const f32x4_t*>(g2 + e);
+    b2v = *reinterpret_cast<const f32x4_t*>(b2 + e);
+  }
   float v[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -123,8 +133,8 @@ __global__ __launch_bounds__(1024) void residual_reduce_ln_v4_kernel(
   }
   *reinterpret_cast<f32x4_t*>(xr) = f32x4_t{v[0], v[1], v[2], v[3]};
   if (!g1) return;
-  ln4(v, D, g1, b1, red);
-  if (g2) ln4(v, D, g2, b2, red);
+  ln4(v, D, g1v, b1v, red);
+  if (g2) ln4(v, D, g2v, b2v, red);
   TO* hr = h + (int64_t)m * ldh + e;
 #pragma unroll
   for (int i = 0; i < 4; ++i) St<TO>::st(hr + i, v[i]);

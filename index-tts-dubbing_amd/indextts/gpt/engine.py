@@ -42,6 +42,18 @@ def pack_skinny(w_t: torch.Tensor) -> torch.Tensor:
     return w.to(torch.bfloat16)
 
 
+def pack_skinny16(w_t: torch.Tensor) -> torch.Tensor:
+    """W^T [N, K] f32 -> 16-column fragment order [N/16][K/32][64 lanes][8] bf16 for
+    itts_decode_gemm16 (lane = 16*q + c holds W^T[16*nt + c][32*s + 8*q : +8]); N zero-padded."""
+    N, K = w_t.shape
+    assert K % 32 == 0
+    Np = (N + 15) // 16 * 16
+    w = torch.zeros(Np, K, dtype=torch.float32)
+    w[:N] = w_t.float()
+    w = w.reshape(Np // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+    return w.to(torch.bfloat16)
+
+
 class _Layer:
     pass
 
@@ -70,6 +82,15 @@ class HipGPT:
         self.mel_emb, self.mel_pos = f32("mel_embedding.weight"), f32("mel_pos_embedding.emb.weight")
         self.ln_f = (f32("gpt.ln_f.weight"), f32("gpt.ln_f.bias"))
         self.final_norm = (f32("final_norm.weight"), f32("final_norm.bias"))
+        # decode-step variants (bf16 product mode), measured at B=32 (scratch/ubench_fusions.py):
+        #  * c_fc on 16-column tiles (itts_decode_gemm16): 6.2 -> 5.5 us, on by default (ITTS_DG16=0: off);
+        #    mel_head stays on 32-column tiles (16-column: 9.5 -> 14.8 us, 513 workgroups too many)
+        #  * attn.c_proj fused into the attention kernel (itts_attn_decode_proj, one f32 partial per
+        #    head): 22.7 us vs 17.0 us for attention + the split-K GEMM at S=283 -- W's 128 KiB per
+        #    workgroup need 256 VGPRs (1 workgroup per CU; at 2 it spills), so off by default
+        #    (ITTS_ATTN_PROJ=1: on)
+        self.fuse_o = dtype == "bf16" and self.D <= 1024 and os.environ.get("ITTS_ATTN_PROJ", "0") == "1"
+        self.use_dg16 = dtype == "bf16" and os.environ.get("ITTS_DG16", "1") != "0"
         self.layers: List[_Layer] = []
         for i in range(self.L):
             p = f"gpt.h.{i}"
@@ -80,7 +101,9 @@ class HipGPT:
             ly.w = {}
             for n, k in (("qkv", "attn.c_attn"), ("o", "attn.c_proj"), ("fc", "mlp.c_fc"), ("proj", "mlp.c_proj")):
                 wt = sd[f"{p}.{k}.weight"].float().t().contiguous()  # HF Conv1D [in, out] -> [out, in]
-                ly.w[n] = self._pack(wt)
+                ly.w[n] = self._pack(wt, sk16=n == "fc")
+            if self.fuse_o:  # attn.c_proj in HF Conv1D [in, out] order (bf16) for the fused attention
+                ly.wo_io = sd[f"{p}.attn.c_proj.weight"].float().to(torch.bfloat16).contiguous().to(dev)
             self.layers.append(ly)
         self.head_w = self._pack(sd["mel_head.weight"].float().contiguous(), igemm=False)
         self.head_b = f32("mel_head.bias")
@@ -93,12 +116,14 @@ class HipGPT:
         self.kv_bytes_per_key = self.L * self.H * 64 * 2 * eb  # the K and V rows of one key, all layers
 
     # ---------------- weights ----------------
-    def _pack(self, wt: torch.Tensor, igemm: bool = True):
+    def _pack(self, wt: torch.Tensor, igemm: bool = True, sk16: bool = False):
         """wt: [N, K] f32 -> dict of device copies for the kernels of this mode."""
         N, K = wt.shape
         if self.mode == "f32":
             return {"f32": wt.to(self.dev), "N": N, "K": K}
         out = {"sk": pack_skinny(wt).to(self.dev), "N": N, "K": K}
+        if sk16 and self.use_dg16 and K % 32 == 0:
+            out["sk16"] = pack_skinny16(wt).to(self.dev)
         if igemm:
             from ..vocoder.bigvgan import pack_taps
             out["ig"] = pack_taps([wt], K, N).to(self.dev)
@@ -217,7 +242,7 @@ class HipGPT:
             "qkv": torch.zeros(self.KSPLIT["qkv"] * B * 3 * D, device=dev),  # c_attn split-K slabs [split][B][3D]
             "o": torch.zeros(Mp, D, dtype=ad, device=dev),
             "f": torch.zeros(Mp, 4 * D, dtype=ad, device=dev),
-            "ws": torch.zeros(max(8, self.KSPLIT["o"], self.KSPLIT["proj"]) * B * D, device=dev),  # split-K partials [split][B][D]
+            "ws": torch.zeros(max(8, self.KSPLIT["o"], self.KSPLIT["proj"], self.H) * B * D, device=dev),  # split-K partials [split][B][D]
             "logits": torch.zeros(B, self.Vp, device=dev),  # row pitch Vp (16-B aligned rows)
             "kc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
             "vc": torch.empty(self.L, B, self.H, self.max_kv, 64, dtype=cdt, device=dev),
@@ -262,7 +287,14 @@ class HipGPT:
                 kq, qkv_bias = self._ksplit(ly.w["qkv"]["K"], self.KSPLIT["qkv"]), ly.b["qkv"]
                 self._dg(h, ly.w["qkv"], B, None, qkv, epi=2, ksplit=kq)
             kc, vc = st["kc"][li], st["vc"][li]
-            if "kv_rows" in st:  # beams: keys read through the lineage table
+            if self.fuse_o:  # attention + attn.c_proj: one f32 partial per head into ws
+                rows = st.get("kv_rows")
+                _hip.check(self.lib.itts_attn_decode_proj(
+                    qkv.data_ptr(), 3 * D, kq, B * 3 * D, _hip.ptr(qkv_bias), kc.data_ptr(), vc.data_ptr(),
+                    kc.stride(0), kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(),
+                    ly.wo_io.data_ptr(), D, st["ws"].data_ptr(), B * D, D, B, self.H, _hip.dtype_code(kc),
+                    _hip.ptr(rows), 0 if rows is None else rows.stride(0), stream), "itts_attn_decode_proj")
+            elif "kv_rows" in st:  # beams: keys read through the lineage table
                 _hip.check(self.lib.itts_attn_decode_rows(
                     qkv.data_ptr(), 3 * D, kq, B * 3 * D, _hip.ptr(qkv_bias), kc.data_ptr(), vc.data_ptr(),
                     kc.stride(0), kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(),
@@ -284,10 +316,13 @@ class HipGPT:
                 else:
                     self._ln(x, h, self.ln_f, self.final_norm, M=B)
                 continue
-            ko = self._ksplit(ly.w["o"]["K"], self.KSPLIT["o"])
-            self._dg(o, ly.w["o"], B, None, st["ws"], epi=2, ksplit=ko)
-            self._reduce(st, ko, ly.b["o"], ly.ln2)
-            self._dg(h, ly.w["fc"], B, ly.b["fc"], f, gelu=True)
+            if self.fuse_o:
+                self._reduce(st, self.H, ly.b["o"], ly.ln2)
+            else:
+                ko = self._ksplit(ly.w["o"]["K"], self.KSPLIT["o"])
+                self._dg(o, ly.w["o"], B, None, st["ws"], epi=2, ksplit=ko)
+                self._reduce(st, ko, ly.b["o"], ly.ln2)
+            self._dgw(h, ly.w["fc"], B, ly.b["fc"], f, gelu=True)
             kp = self._ksplit(ly.w["proj"]["K"], self.KSPLIT["proj"])
             self._dg(f, ly.w["proj"], B, None, st["ws"], epi=2, ksplit=kp)
             if nxt is not None:
@@ -297,7 +332,7 @@ class HipGPT:
         if self.mode == "f32":
             self._gemm(h[:B], self.head_w, st["logits"], bias=self.head_b)
         else:
-            self._dg(h, self.head_w, B, self.head_b, st["logits"])
+            self._dgw(h, self.head_w, B, self.head_b, st["logits"])
         if "kv_rows" in st:
             self._beam_step(st, 1)
         else:
@@ -316,6 +351,14 @@ class HipGPT:
         while ks > 1 and (K // 16) % ks:
             ks //= 2
         return ks
+
+    def _dgw(self, A, w, M, bias, Y, gelu=False):
+        """store-epilogue projection (c_fc + gelu, mel_head): 16-column tiles when packed for them."""
+        if "sk16" not in w:
+            return self._dg(A, w, M, bias, Y, gelu=gelu)
+        _hip.check(self.lib.itts_decode_gemm16(
+            A.data_ptr(), A.stride(0), w["sk16"].data_ptr(), w["K"], w["N"], M, _hip.ptr(bias), int(gelu),
+            Y.data_ptr(), Y.stride(0), _hip.dtype_code(Y), _hip.stream_ptr()), "itts_decode_gemm16")
 
     def _dg(self, A, w, M, bias, Y, ln=None, ln2=None, gelu=False, epi=0, ksplit=1):
         """itts_decode_gemm: Y = act(prologue(A) @ W^T + bias) (epi 0), Y += ... (epi 1), or split-K
@@ -481,7 +524,7 @@ class HipGPT:
         if self.mode == "f32":
             self._gemm(st["h"][:B], self.head_w, st["logits"], bias=self.head_b)
         else:
-            self._dg(st["h"], self.head_w, B, self.head_b, st["logits"])
+            self._dgw(st["h"], self.head_w, B, self.head_b, st["logits"])
         self._sample(st, 0, min_new, penalty)
         ln["graph_ok"] = False
         if use_graph:
@@ -618,7 +661,7 @@ class HipGPT:
         if self.mode == "f32":
             self._gemm(st["h"][:R], self.head_w, st["logits"], bias=self.head_b)
         else:
-            self._dg(st["h"], self.head_w, R, self.head_b, st["logits"])
+            self._dgw(st["h"], self.head_w, R, self.head_b, st["logits"])
         self._beam_step(st, 0)
         gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling)
         graph_ok = use_graph and max_new_tokens > 1

@@ -179,3 +179,21 @@ def test_graph_replay_across_calls_matches_eager(golden):
         assert torch.equal(a, b), call
         outs.append(a)
     assert not torch.equal(outs[0], outs[1])
+
+
+def test_bf16_fused_attn_proj_teacher_forced_ids(golden, monkeypatch):
+    """Opt-in decode variant (ITTS_ATTN_PROJ=1: attn.c_proj fused into the attention kernel, one f32
+    partial per head): the same teacher-forced parity bar as the default path (ids equal wherever the
+    reference top-1/top-2 margin > 0.1)."""
+    monkeypatch.setenv("ITTS_ATTN_PROJ", "1")
+    from indextts.gpt.engine import HipGPT
+    eng = HipGPT(_sd("tiny"), _cfg("tiny").gpt, "cuda", dtype="bf16", max_kv=256)
+    assert eng.fuse_o
+    conds = torch.from_numpy(golden["tiny_gpt_conds"])
+    text = torch.from_numpy(golden["tiny_gpt_text"])
+    ref = torch.from_numpy(golden["tiny_gpt_codes_forced"])
+    n = ref.shape[1]
+    got = eng.generate(conds.cuda(), text.cuda(), n, min_new_tokens=n, forced_codes=ref.cuda()).cpu()
+    sure = _margins("tiny", conds, text, ref) > 0.1
+    mism = (got[0].numpy() != ref[0].numpy()) & sure
+    assert not mism.any(), np.nonzero(mism)

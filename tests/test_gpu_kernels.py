@@ -77,10 +77,47 @@ def test_decode_gemm(K, N, M, mode):
         assert torch.equal(Y[M:].float().cpu(), Y0[M:].to(Y.dtype).float())
 
 
-def test_residual_reduce_ln_matches_torch():
+@pytest.mark.parametrize("K,N,M,gelu", [(1024, 4096, 32, True), (1024, 8194, 32, False), (512, 96, 3, False),
+                                        (1024, 1000, 45, True)])
+def test_decode_gemm16(K, N, M, gelu):
+    """16-column decode GEMM (c_fc + gelu -> bf16, mel_head -> f32) vs torch fp32 on the same
+    bf16-rounded operands: |err| <= 1e-2 * (|A| @ |W|^T) (+ bf16 output rounding with gelu); rows
+    beyond M untouched."""
+    from indextts.gpt.engine import pack_skinny16
     _hip, lib = _lib()
-    torch.manual_seed(0)
-    B, D, S = 32, 1024, 8
+    torch.manual_seed(K + N + M)
+    Mp = (M + 31) // 32 * 32
+    W = torch.randn(N, K) / K ** 0.5
+    bias = torch.randn(N) * 0.1
+    X = torch.randn(Mp, K)
+    A = X[:M].to(torch.bfloat16).float()
+    Wq = W.to(torch.bfloat16).float()
+    ref = A @ Wq.t() + bias
+    if gelu:
+        ref = F.gelu(ref, approximate="tanh")
+    Y0 = torch.randn(Mp, N)
+    Y = Y0.clone().to(torch.bfloat16 if gelu else torch.float32).cuda()
+    a_dev, w_dev, b_dev = X.to(torch.bfloat16).cuda(), pack_skinny16(W).cuda(), bias.cuda()
+    _hip.check(lib.itts_decode_gemm16(a_dev.data_ptr(), K, w_dev.data_ptr(), K, N, M, b_dev.data_ptr(), int(gelu),
+                                      Y.data_ptr(), N, _hip.dtype_code(Y), _hip.stream_ptr()), "decode_gemm16")
+    torch.cuda.synchronize()
+    got = Y[:M].float().cpu()
+    assert torch.isfinite(got).all()
+    scale = (A.abs() @ Wq.abs().t()) + 1e-3
+    tol = (2e-2 if gelu else 1e-2) * scale + (1e-2 if gelu else 0)
+    err = (got - ref).abs()
+    assert bool((err <= tol).all()), float((err / scale).max())
+    if Mp > M:
+        assert torch.equal(Y[M:].float().cpu(), Y0[M:].to(Y.dtype).float())
+
+
+@pytest.mark.parametrize("S", [8, 16])
+def test_residual_reduce_ln_matches_torch(S):
+    """x += bias + the S split partials in order (S = 16: one per head from itts_attn_decode_proj);
+    h = LN2(LN1(x)) in bf16."""
+    _hip, lib = _lib()
+    torch.manual_seed(S)
+    B, D = 32, 1024
     x = torch.randn(B, D)
     part = torch.randn(S, B, D)
     bias = torch.randn(D)
@@ -148,6 +185,59 @@ def test_attn_decode_matches_torch(S, cache, nsplit):
     keep = torch.ones(smax, dtype=torch.bool)
     keep[kidx] = False
     assert torch.equal(kd[:, :, keep].cpu(), kc[:, :, keep]) and torch.equal(vd[:, :, keep].cpu(), vc[:, :, keep])
+
+
+@pytest.mark.parametrize("S,rows", [(37, False), (300, False), (513, True)])
+def test_attn_decode_proj_matches_torch(S, rows):
+    """Attention with attn.c_proj fused (itts_attn_decode_proj): part[h][b] = o_h[b] @ W[64h : 64h+64]
+    with o_h the head's f32 attention output and W the bf16 c_proj weight in HF Conv1D [in, out]
+    order; vs torch fp32 on the same bf16 cache and weights: |err| <= 2e-3 * (|o| @ |W|) + 1e-5.  The
+    lineage-table variant (rows=True, identity table) reads the same keys.  This step's k/v are
+    appended to the cache as in itts_attn_decode."""
+    _hip, lib = _lib()
+    torch.manual_seed(S + 1)
+    B, H, smax, nsplit = 5, 16, S + 8, 2
+    D = 64 * H
+    kc = (torch.randn(B, H, smax, 64) * 0.5).to(torch.bfloat16)
+    vc = torch.randn(B, H, smax, 64).to(torch.bfloat16)
+    parts = torch.randn(nsplit, B, 3 * D) / nsplit ** 0.5
+    bias = torch.randn(3 * D) * 0.1
+    qkv = bias.expand(B, -1).clone()
+    for sp in range(nsplit):
+        qkv = qkv + parts[sp]
+    W = (torch.randn(D, D) / D ** 0.5).to(torch.bfloat16)  # [in, out]
+    pad = torch.tensor([0, 3, 0, min(7, S - 1), 1], dtype=torch.int32).clamp(max=S - 1)
+    kv_base, t = S - 1 - 2, 2
+    kd, vd = kc.clone().cuda(), vc.clone().cuda()
+    part = torch.full((H, B, D), float("nan")).cuda()
+    tst = torch.tensor([t, 0, 0, 0], dtype=torch.int32).cuda()
+    qkv_d, pad_d, bias_d, w_d = parts.cuda(), pad.cuda(), bias.cuda(), W.cuda()
+    kvr = torch.arange(B, dtype=torch.int32)[:, None].expand(B, smax).contiguous().cuda() if rows else None
+    _hip.check(lib.itts_attn_decode_proj(qkv_d.data_ptr(), 3 * D, nsplit, B * 3 * D, bias_d.data_ptr(), kd.data_ptr(),
+                                         vd.data_ptr(), kd.stride(0), kd.stride(1), smax, pad_d.data_ptr(), kv_base,
+                                         tst.data_ptr(), w_d.data_ptr(), D, part.data_ptr(), B * D, D, B, H,
+                                         _hip.BF16, _hip.ptr(kvr), smax if rows else 0, _hip.stream_ptr()),
+               "attn_decode_proj")
+    torch.cuda.synchronize()
+    kidx = S - 1
+    q = qkv[:, :D].view(B, H, 64)
+    kn, vn = qkv[:, D:2 * D].view(B, H, 64), qkv[:, 2 * D:].view(B, H, 64)
+    kr, vr = kc.float().clone(), vc.float().clone()
+    kr[:, :, kidx], vr[:, :, kidx] = kn, vn
+    o = torch.zeros(B, H, 64)
+    for b in range(B):
+        p0 = int(pad[b])
+        sc = torch.einsum("hd,hsd->hs", q[b], kr[b, :, p0:kidx + 1]) / 8.0
+        o[b] = torch.einsum("hs,hsd->hd", sc.softmax(-1), vr[b, :, p0:kidx + 1])
+    Wf = W.float().view(H, 64, D)
+    ref = torch.einsum("bhd,hdn->hbn", o, Wf)
+    scale = torch.einsum("bhd,hdn->hbn", o.abs(), Wf.abs())
+    got = part.cpu()
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs()
+    assert bool((err <= 2e-3 * scale + 1e-5).all()), float(err.max())
+    assert torch.equal(kd[:, :, kidx].cpu(), kn.to(torch.bfloat16)) and torch.equal(vd[:, :, kidx].cpu(),
+                                                                                     vn.to(torch.bfloat16))
 
 
 @pytest.mark.parametrize("mode", ["bf16", "f32"])
