@@ -230,8 +230,8 @@ def main():
         d_ms = sum(a.elapsed_time(b) for a, b, _, _ in step_ev)
         d_bytes = sum(tts.gpt.step_weight_bytes + keys * tts.gpt.kv_bytes_per_key for _, _, _, keys in step_ev)
         gbs = d_bytes / (d_ms * 1e-3) / 1e9
-        dec = {"kernel": "GPT decode step (hipGraph: 20 x [c_attn GEMM, attention, c_proj GEMM, reduce+LN, "
-                         "c_fc GEMM, mlp.c_proj GEMM, reduce+LN] + mel_head GEMM + sampler)", "bound": "hbm",
+        dec = {"kernel": "GPT decode step (hipGraph: 20 x [c_attn GEMM, attention, c_proj GEMM (split-K 8), reduce+LN, "
+                         "c_fc GEMM (16-column tiles), mlp.c_proj GEMM, reduce+LN] + mel_head GEMM + sampler)", "bound": "hbm",
                "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
                "traffic": None, "launches": len(step_ev), "avg_launch_us": round(1e3 * d_ms / len(step_ev), 2),
                "algorithmic_bytes_per_launch": round(d_bytes / len(step_ev)), "share_of_step": round(d_ms / (1e3 * dt), 3)}
