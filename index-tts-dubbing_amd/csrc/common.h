@@ -18,9 +18,9 @@ enum ItTsDtype { ITTS_F32 = 0, ITTS_BF16 = 1 };
 // ---- bf16 <-> f32 (bf16 carried as raw uint16_t) ----
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);  // round to nearest even (NaN payloads may collapse: not produced here)
-  return (uint16_t)(u >> 16);
+  // hardware round-to-nearest-even (v_cvt_pk_bf16_f32 on gfx950: one instruction instead of four
+  // integer ops; bit-identical to the integer RNE for every finite value)
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
 }
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
 
