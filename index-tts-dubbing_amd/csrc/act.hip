@@ -43,7 +43,10 @@ __device__ __forceinline__ float snake(float u, float a_rev, float inv_b) {
   return fmaf(inv_b, s * s, u);
 }
 
-template <typename TI, typename TO, bool VEC>
+// VOUT (bf16 channel-last output, C % 8 == 0): outputs go to an LDS tile [TT][CT] bf16 as they are
+// computed and leave as 16-B row vectors after one barrier (2 wide stores per thread instead of 16
+// 2-byte stores, one per output)
+template <typename TI, typename TO, bool VEC, bool VOUT>
 __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
   extern __shared__ __attribute__((aligned(16))) float xs[];
   const int b = blockIdx.z;
@@ -96,11 +99,15 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
   }
   __syncthreads();
 
+  uint16_t* ys = reinterpret_cast<uint16_t*>(xs + rows * CT);  // VOUT: [TT][CT] bf16 output tile
   const int c = threadIdx.x % CT, sub = threadIdx.x / CT;
   const int ch = c0 + c;
-  if (sub >= nsub || ch >= p.C) return;
   const int ts = t0 + sub * kTO;
-  if (ts >= len) return;
+  auto emit = [&](int t, float o) {
+    if constexpr (VOUT) ys[(t - t0) * CT + c] = f2bf(o);
+    else St<TO>::st(y + (int64_t)t * p.syt + (int64_t)ch * p.syc, o);
+  };
+  if (sub < nsub && ch < p.C && ts < len) {
   float f[12], g[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) { f[k] = 2.0f * p.up[k]; g[k] = p.down[k]; }  // x2: the up-sampler gain (exact)
@@ -130,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
       float o = 0.f;
 #pragma unroll
       for (int k = 0; k < 12; ++k) o = fmaf(g[k], v[2 * i + k], o);
-      St<TO>::st(y + (int64_t)(ts + i) * p.syt + (int64_t)ch * p.syc, o);
+      emit(ts + i, o);
     }
   } else {
     // edge chunk: explicit two-level replicate clamping (x level and activated-signal level)
@@ -149,19 +156,41 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
         }
         o = fmaf(g[k], snake(acc, a, inv_b), o);
       }
-      St<TO>::st(y + (int64_t)t * p.syt + (int64_t)ch * p.syc, o);
+      emit(t, o);
+    }
+  }
+  }  // active thread
+  if constexpr (VOUT) {
+    __syncthreads();
+    const int nrow = min(TT, len - t0), cv = CT / 8;
+    for (int v = threadIdx.x; v < nrow * cv; v += kThreads) {
+      const int r = v / cv, cc = (v - r * cv) * 8;
+      if (c0 + cc < p.C)
+        *reinterpret_cast<u32x4_t*>(y + (int64_t)(t0 + r) * p.syt + c0 + cc) =
+            *reinterpret_cast<const u32x4_t*>(ys + r * CT + cc);
     }
   }
 }
 
 template <typename TI, typename TO>
-void launch(const ActArgs& a, bool vec, hipStream_t s) {
+void launch(const ActArgs& a, bool vec, bool vout, hipStream_t s) {
   dim3 grid((a.T + a.nsub * kTO - 1) / (a.nsub * kTO), (a.C + a.CT - 1) / a.CT, a.B);
-  size_t lds = sizeof(float) * (size_t)(a.nsub * kTO + 2 * kHalo) * a.CT;
+  const int TT = a.nsub * kTO;
+  size_t lds = sizeof(float) * (size_t)(TT + 2 * kHalo) * a.CT;
+  if constexpr (sizeof(TO) == 2) {
+    if (vout) {
+      lds += sizeof(uint16_t) * (size_t)TT * a.CT;
+      if (vec)
+        hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, true, true>), grid, dim3(kThreads), lds, s, a);
+      else
+        hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, false, true>), grid, dim3(kThreads), lds, s, a);
+      return;
+    }
+  }
   if (vec)
-    hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, true>), grid, dim3(kThreads), lds, s, a);
+    hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, true, false>), grid, dim3(kThreads), lds, s, a);
   else
-    hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, false>), grid, dim3(kThreads), lds, s, a);
+    hipLaunchKernelGGL((aa_snakebeta_kernel<TI, TO, false, false>), grid, dim3(kThreads), lds, s, a);
 }
 
 }  // namespace
@@ -185,10 +214,13 @@ extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, 
   // vectorised staging: channel-last bf16 input, 16-B aligned rows
   const bool vec = dtype_in == ITTS_BF16 && x_sc == 1 && C % 8 == 0 && x_st % 8 == 0 && x_sb % 8 == 0 &&
                    (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, s);
-  else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, false, s);
-  else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, false, s);
-  else launch<uint16_t, float>(a, vec, s);
+  // vectorised output through LDS: channel-last bf16 output, 16-B aligned rows
+  const bool vout = dtype_out == ITTS_BF16 && y_sc == 1 && C % 8 == 0 && y_st % 8 == 0 && y_sb % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+  if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, vout, s);
+  else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, false, false, s);
+  else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, false, vout, s);
+  else launch<uint16_t, float>(a, vec, false, s);
   return itts::check_launch(fn);
 }
 
