@@ -414,7 +414,10 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(const float* __r
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
   float m = -INFINITY, l = 0.f;
   const int kmax = min(q_hi, len);  // keys [p0, kmax) can be attended by this block
-  for (int k0 = (p0 / kFK) * kFK; k0 < kmax; k0 += kFK) {
+  // key tiles start at the first valid key p0 (not at a multiple of 32): the partition of a
+  // sequence's keys into tiles -- and so its f32 rounding -- does not depend on its left padding
+  // (batch invariance: a row decodes the same ids in a padded batch as alone, padding_test.py)
+  for (int k0 = p0; k0 < kmax; k0 += kFK) {
     __syncthreads();  // previous tile fully consumed
     {  // stage K [key][dim] and V^T [dim][key] (bf16); write the cache for keys of this block's range
       const int kk = tid >> 3, d0 = (tid & 7) * 8, key = k0 + kk;

@@ -109,6 +109,7 @@ class HipGPT:
         self.head_b = f32("mel_head.bias")
         self._lanes = {}  # lane index -> decode state, captured graph, stream
         self.step_events = None  # set to a list to time every decode step with HIP events (bench.py)
+        self.logits_trace = None  # set to a list to record every step's raw logits [B, V] (tests)
         # algorithmic HBM bytes of one decode step: every weight byte once (+ per-key KV bytes)
         eb = 2 if dtype == "bf16" else 4
         self.step_weight_bytes = sum(eb * ly.w[n]["N"] * ly.w[n]["K"] for ly in self.layers for n in ly.w) \
@@ -452,6 +453,8 @@ class HipGPT:
                                  repetition_penalty, use_graph and max_new_tokens > 1, gkey)
             work.append(ln)
         steps = 1
+        trace = self.logits_trace  # optional instrumentation (tests): raw f32 logits of every step
+        assert trace is None or len(work) == 1, "logits tracing needs a single lane"
         ev = self.step_events  # optional instrumentation: HIP events around each lane's step
         keys0 = [int((r1 - r0) * (s + 2)) - int(pad[r0:r1].sum()) for r0, r1 in self._lane_bounds(B, lanes)] \
             if ev is not None else None
@@ -470,6 +473,8 @@ class HipGPT:
                         e1.record()
                         # keys attended this step, summed over the lane's rows: s + 2 + r - pad_b
                         ev.append((e0, e1, ln["st"]["B"], keys0[li] + ln["st"]["B"] * (steps - 1)))
+                    if trace is not None:
+                        trace.append(ln["st"]["logits"][:, : self.V].clone())
             steps += 1
             if steps % check_every == 0:
                 done = True
@@ -526,6 +531,8 @@ class HipGPT:
         else:
             self._dgw(st["h"], self.head_w, B, self.head_b, st["logits"])
         self._sample(st, 0, min_new, penalty)
+        if self.logits_trace is not None:  # the prefill's logits (before the capture's warm-up step)
+            self.logits_trace.append(st["logits"][:, : self.V].clone())
         ln["graph_ok"] = False
         if use_graph:
             if ln["graph"] is None or ln["graph"][1] != gkey:
