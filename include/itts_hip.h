@@ -121,6 +121,17 @@ int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed, int K, in
  * workgroups of itts_decode_gemm, half the weight bytes each. */
 int itts_decode_gemm16(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M, const float* bias,
                        int gelu, void* y, int64_t ldy, int out_dtype, void* stream);
+/* 16-column decode GEMM with the LayerNorm FOLDED in and a residual epilogue (product decode step:
+ * five launches per layer).  With u != NULL: y = rstd * (a @ W'^T - mean * u) + c, where the row
+ * statistics (mean, rstd with eps) of `a` are taken from the same A fragments the MFMAs consume,
+ * W' = diag(ln.g) W (bf16), u = column sums of W', c = ln.b^T W + bias: exactly LN(a) @ W + bias
+ * (HF ln_1 -> c_attn / ln_2 -> c_fc, modeling_gpt2.py:246-306).  With u == NULL: y = a @ W^T + c.
+ * epi 0: store act(y) (gelu_tanh if gelu) as out_dtype; epi 1 (attn.c_proj / mlp.c_proj): residual,
+ * y is the f32 stream x[M][ldy]: x += y, and xh[M][ldxh] = bf16(x) (the next A operand).
+ * nwaves = 8 or 16 per workgroup. */
+int itts_decode_gemm16x(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M, const float* c,
+                        const float* u, float eps, int gelu, int epi, void* y, int64_t ldy, int out_dtype, void* xh,
+                        int64_t ldxh, int nwaves, void* stream);
 /* One decode step of 16x64 causal attention per row: appends this step's k/v at position
  * kv_base + tstate[0] of the cache [B][H][smax][64] and attends over the valid (pad-masked,
  * quirk Q2) prefix.  HF modeling_gpt2.py:54-72,185-225 with the additive padding mask. */

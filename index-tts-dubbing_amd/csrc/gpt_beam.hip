@@ -571,6 +571,13 @@ __global__ __launch_bounds__(kT) void beam_select_kernel(SelArgs p) {
         p.x[(int64_t)r * p.D + e] = vals[i];
         s += vals[i];
       }
+    if (!p.g) {  // ln_1 folded into the c_attn GEMM: h = x, rounded
+      TH* hr = reinterpret_cast<TH*>(p.h) + (int64_t)r * p.D;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i < n) St<TH>::st(hr + threadIdx.x + kT * i, vals[i]);
+      continue;
+    }
     const float mean = block_reduce<kT>(s, rv, false) / p.D;
     float q = 0.f;
 #pragma unroll
@@ -625,8 +632,8 @@ extern "C" int itts_beam_select(const float* cand_key, const float* cand_score, 
   ITTS_REQUIRE(B >= 0 && num_beams >= 2 && num_beams <= kMaxBeams && D > 0 && D <= kT * 16, fn, "bad sizes");
   if (B == 0) return 0;
   ITTS_REQUIRE(cand_key && cand_score && cand_tok && tstate && done && beam_score && codes && seen && kv_rows &&
-                   hyp_score && hyp_len && hyp_codes && hyp_n && hyp_order && hyp_worst && emb && pos_emb && ln_g &&
-                   ln_b && x && h && (n_base == 0 || base_ids),
+                   hyp_score && hyp_len && hyp_codes && hyp_n && hyp_order && hyp_worst && emb && pos_emb && (!ln_g || ln_b) &&
+                   x && h && (n_base == 0 || base_ids),
                fn, "null pointer");
   ITTS_REQUIRE(n_base >= 0 && num_beams * n_base <= kT, fn, "too many base ids");
   ITTS_REQUIRE(max_col >= 1 && max_col <= ldc && kv_base + max_col <= ld_rows, fn, "bad step capacity");

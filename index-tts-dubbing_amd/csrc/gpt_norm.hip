@@ -132,7 +132,14 @@ __global__ __launch_bounds__(1024) void residual_reduce_ln_v4_kernel(
     v[i] = acc[i] + p;
   }
   *reinterpret_cast<f32x4_t*>(xr) = f32x4_t{v[0], v[1], v[2], v[3]};
-  if (!g1) return;
+  if (!g1) {  // no LayerNorm (folded into the consumer GEMM): h = x, rounded
+    if (h) {
+      TO* hr = h + (int64_t)m * ldh + e;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) St<TO>::st(hr + i, v[i]);
+    }
+    return;
+  }
   ln4(v, D, g1v, b1v, red);
   if (g2) ln4(v, D, g2v, b2v, red);
   TO* hr = h + (int64_t)m * ldh + e;
@@ -162,9 +169,9 @@ __global__ __launch_bounds__(kT) void residual_reduce_ln_kernel(float* __restric
       xr[e] = v[i];
     }
   }
-  if (g1) {
-    ln_inplace(v, n, D, g1, b1, red);
-    if (g2) ln_inplace(v, n, D, g2, b2, red);
+  if (g1 || h) {
+    if (g1) ln_inplace(v, n, D, g1, b1, red);
+    if (g1 && g2) ln_inplace(v, n, D, g2, b2, red);
     TO* hr = h + (int64_t)m * ldh;
 #pragma unroll
     for (int i = 0; i < kMaxPer; ++i)

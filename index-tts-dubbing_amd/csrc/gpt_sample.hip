@@ -61,6 +61,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __device__ __forceinline__ float uniform01(uint64_t key) { return ((float)(mix64(key) >> 40) + 0.5f) * 5.9604645e-8f; }
 
 // record the chosen token, then write x = mel_emb[tok] + mel_pos[col + pos_delta] and h = ln_1(x)
+// (h = x when g is null: ln_1 is folded into the c_attn GEMM)
 template <typename TH>
 __device__ __forceinline__ void commit_and_embed(int b, int ii, int col, int V, int stop, uint8_t* sr, uint8_t* done,
                                                  int32_t* codes, int64_t ldc, const int32_t* forced,
@@ -93,6 +94,12 @@ __device__ __forceinline__ void commit_and_embed(int b, int ii, int col, int V, 
       s += v[i];
     }
   if (!h) return;
+  if (!g) {  // LayerNorm folded into the consumer GEMM (itts_decode_gemm16x): h = x, rounded
+#pragma unroll
+    for (int i = 0; i < kMaxPer; ++i)
+      if (i < n) St<TH>::st(h + (int64_t)b * D + threadIdx.x + kT * i, v[i]);
+    return;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   s = wave_sum(s);
   __syncthreads();
@@ -328,7 +335,7 @@ int launch_sample(const char* fn, SampleArgs& p, int h_dtype, int B, bool do_sam
   if (B == 0) return 0;
   ITTS_REQUIRE(p.logits && p.seen && p.done && p.codes && p.tstate, fn, "null pointer");
   ITTS_REQUIRE(!p.x || (p.emb && p.pos_emb), fn, "embedding output needs the embedding tables");
-  ITTS_REQUIRE(!p.h || (p.x && p.g && p.bta), fn, "h output needs x and ln_1 params");
+  ITTS_REQUIRE(!p.h || (p.x && (!p.g || p.bta)), fn, "h output needs x (and ln_1 bias with ln_1 weight; no ln_1: h = x)");
   hipStream_t s = itts::as_stream(stream);
   ITTS_REQUIRE(p.ldl >= p.V, fn, "row pitch ldl < V");
   if (!do_sample) {

@@ -54,6 +54,8 @@ SIGNATURES = {
     "itts_attn_decode_proj": (_c_i, [_vp, _c_i64, _c_i, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _c_i, _vp, _c_i, _vp,
                                      _vp, _c_i, _vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _vp, _c_i64, _vp]),
     "itts_decode_gemm16": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _c_i, _vp, _c_i64, _c_i, _vp]),
+    "itts_decode_gemm16x": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _c_f, _c_i, _c_i, _vp, _c_i64, _c_i,
+                                   _vp, _c_i64, _c_i, _vp]),
     "itts_beam_candidates": (_c_i, [_vp, _c_i64, _c_i, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_f, _c_i, _c_f, _c_i, _c_f,
                                     _c_i, _vp, _vp, _vp, _c_i, _vp]),
     "itts_beam_select": (_c_i, [_vp, _vp, _vp, _c_i, _c_i, _c_i, _c_i, _c_f, _vp, _c_i, _vp, _vp, _vp, _c_i64, _vp,

@@ -1,8 +1,9 @@
 """Speech-prompt conditioning: conformer encoder + perceiver resampler -> ``conds [B, 32, D]``.
 
 Runs once per prompt (cached by the caller, quirk Q6), so it is PyTorch-ROCm code on the device
-rather than a hand-written kernel target (§8(f) item 2 is the plan to
-move it to HIP).  Functional restatement over the reference state-dict, device agnostic.
+rather than a hand-written kernel target.  Its convolutions are explicit
+im2col GEMMs (``utils/convgemm.py``: deterministic without MIOpen's naive direct kernel, §8(f) item 2).
+Functional restatement over the reference state-dict, device agnostic.
 
 Reference behaviour followed (file:line in the reference tree):
   * ``UnifiedVoice.get_conditioning`` conformer_perceiver branch  gpt/model.py:496-502
@@ -21,6 +22,8 @@ import math
 
 import torch
 import torch.nn.functional as F
+
+from ..utils.convgemm import conv1d, conv2d_s2
 
 
 def _lin(x, sd, name, bias=True):
@@ -51,12 +54,12 @@ def _rel_pos_mha(x, sd, p, heads, mask, pos_emb):
 def _conv_module(x, sd, p, mask):
     C = x.shape[-1]
     h = x.transpose(1, 2).masked_fill(~mask, 0.0)  # [B, C, T]
-    h = F.conv1d(h, sd[p + ".pointwise_conv1.weight"], sd[p + ".pointwise_conv1.bias"])
+    h = conv1d(h, sd[p + ".pointwise_conv1.weight"], sd[p + ".pointwise_conv1.bias"])
     h = F.glu(h, dim=1)
     w = sd[p + ".depthwise_conv.weight"]
-    h = F.conv1d(h, w, sd[p + ".depthwise_conv.bias"], padding=(w.shape[-1] - 1) // 2, groups=C)
+    h = conv1d(h, w, sd[p + ".depthwise_conv.bias"], padding=(w.shape[-1] - 1) // 2, groups=C)
     h = F.silu(_ln(h.transpose(1, 2), sd, p + ".norm")).transpose(1, 2)
-    h = F.conv1d(h, sd[p + ".pointwise_conv2.weight"], sd[p + ".pointwise_conv2.bias"])
+    h = conv1d(h, sd[p + ".pointwise_conv2.weight"], sd[p + ".pointwise_conv2.bias"])
     return h.masked_fill(~mask, 0.0).transpose(1, 2)
 
 
@@ -67,7 +70,7 @@ def conformer_encode(sd, mel, mel_lengths, heads: int, num_blocks: int, prefix="
     valid = torch.arange(T, device=x.device)[None, :] < mel_lengths.to(x.device)[:, None]
     mask = valid.unsqueeze(1)
     p = prefix + ".embed"
-    h = F.relu(F.conv2d(x.unsqueeze(1), sd[p + ".conv.0.weight"], sd[p + ".conv.0.bias"], stride=2))
+    h = F.relu(conv2d_s2(x.unsqueeze(1), sd[p + ".conv.0.weight"], sd[p + ".conv.0.bias"]))
     b, c, t, f = h.shape
     h = _lin(h.transpose(1, 2).reshape(b, t, c * f), sd, p + ".out.0")
     C = h.shape[-1]

@@ -54,6 +54,25 @@ def pack_skinny16(w_t: torch.Tensor) -> torch.Tensor:
     return w.to(torch.bfloat16)
 
 
+def fold_ln_weights(w_io, bias, ln, device):
+    """Operands of itts_decode_gemm16x for HF Conv1D weight ``w_io`` [in=K, out=N] (+ bias [N]) fed by
+    LayerNorm ``ln`` = (g, b) (None: no LayerNorm): W' = diag(g) W rounded to bf16 and packed on
+    16-column tiles, u = column sums of the ROUNDED W' (so the kernel's mean term cancels exactly what
+    its MFMAs accumulated), c = b^T W + bias (float64 accumulation)."""
+    w = _t(w_io).double()
+    bias = _t(bias).double()
+    if ln is None:
+        wt = w.t().float()
+        return {"w16": pack_skinny16(wt).to(device), "u": None, "c": bias.float().to(device),
+                "N": wt.shape[0], "K": wt.shape[1]}
+    g, b = _t(ln[0]).double(), _t(ln[1]).double()
+    wp = (w * g[:, None]).t().float().to(torch.bfloat16)  # W'^T [N, K]
+    u = wp.double().sum(1)
+    c = b @ w + bias
+    return {"w16": pack_skinny16(wp.float()).to(device), "u": u.float().to(device), "c": c.float().to(device),
+            "N": wp.shape[0], "K": wp.shape[1]}
+
+
 class _Layer:
     pass
 
@@ -91,6 +110,12 @@ class HipGPT:
         #    (ITTS_ATTN_PROJ=1: on)
         self.fuse_o = dtype == "bf16" and self.D <= 1024 and os.environ.get("ITTS_ATTN_PROJ", "0") == "1"
         self.use_dg16 = dtype == "bf16" and os.environ.get("ITTS_DG16", "1") != "0"
+        #  * LayerNorm folded into the consumer GEMMs + residual epilogues (itts_decode_gemm16x): five
+        #    launches per layer instead of seven (ITTS_LN_FOLD=0: the split-K + reduce/LN path)
+        self.fold = dtype == "bf16" and not self.fuse_o and os.environ.get("ITTS_LN_FOLD", "1") != "0"
+        #  * mlp.c_proj: split-K 8 + reduce launch (default) or one full-K launch of 64 workgroups with
+        #    the residual epilogue (ITTS_PROJ_FULLK=1)
+        self.proj_fullk = self.fold and os.environ.get("ITTS_PROJ_FULLK", "0") == "1"
         self.layers: List[_Layer] = []
         for i in range(self.L):
             p = f"gpt.h.{i}"
@@ -102,6 +127,14 @@ class HipGPT:
             for n, k in (("qkv", "attn.c_attn"), ("o", "attn.c_proj"), ("fc", "mlp.c_fc"), ("proj", "mlp.c_proj")):
                 wt = sd[f"{p}.{k}.weight"].float().t().contiguous()  # HF Conv1D [in, out] -> [out, in]
                 ly.w[n] = self._pack(wt, sk16=n == "fc")
+            if self.fold:  # itts_decode_gemm16x operands (LayerNorm folded / residual epilogue)
+                ly.wx = {}
+                for n, k, ln in (("qkv", "attn.c_attn", ly.ln1), ("o", "attn.c_proj", None),
+                                 ("fc", "mlp.c_fc", ly.ln2), ("proj", "mlp.c_proj", None)):
+                    ly.wx[n] = fold_ln_weights(sd[f"{p}.{k}.weight"], sd[f"{p}.{k}.bias"],
+                                               None if ln is None else (sd[f"{p}.ln_{1 if n == 'qkv' else 2}.weight"],
+                                                                        sd[f"{p}.ln_{1 if n == 'qkv' else 2}.bias"]),
+                                               dev)
             if self.fuse_o:  # attn.c_proj in HF Conv1D [in, out] order (bf16) for the fused attention
                 ly.wo_io = sd[f"{p}.attn.c_proj.weight"].float().to(torch.bfloat16).contiguous().to(dev)
             self.layers.append(ly)
@@ -133,9 +166,9 @@ class HipGPT:
     # ---------------- conditioning + inputs ----------------
     @torch.no_grad()
     def conditioning(self, mel: torch.Tensor, mel_lengths=None) -> torch.Tensor:
-        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):  # run-to-run identical
-            return get_conditioning(self.sd_cond, self.cfg, mel.to(self.dev).float(),
-                                    None if mel_lengths is None else mel_lengths.to(self.dev))
+        # convolutions are GEMMs (utils/convgemm.py): run-to-run identical without MIOpen
+        return get_conditioning(self.sd_cond, self.cfg, mel.to(self.dev).float(),
+                                None if mel_lengths is None else mel_lengths.to(self.dev))
 
     def prepare_inputs(self, conds: torch.Tensor, text_ids: torch.Tensor):
         """``prepare_gpt_inputs`` (gpt/model.py:591-654): strip ids 0/1, [0]+ids+[1], left zero pad.
@@ -255,6 +288,13 @@ class HipGPT:
         }
         return st
 
+    def _embed_ln(self):
+        """LayerNorm the sampler applies to the next token's embedding (h = ln_1(x) of layer 0), or
+        none when ln_1 is folded into c_attn (h = bf16 x)."""
+        if self.fold:
+            return None, None
+        return self.layers[0].ln1[0].data_ptr(), self.layers[0].ln1[1].data_ptr()
+
     def _sample(self, st, col_delta, min_new, penalty):
         smp = st.get("sampling")
         if smp is not None:  # (temperature, top_k, top_p); the seed is device state (t[2:4])
@@ -262,7 +302,7 @@ class HipGPT:
                 st["logits"].data_ptr(), self.Vp, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
                 st["codes"].data_ptr(), st["max_new"], st["t"].data_ptr(), col_delta, int(min_new), self.stop_mel,
                 float(penalty), float(smp[0]), int(smp[1]), float(smp[2]), self.mel_emb.data_ptr(),
-                self.mel_pos.data_ptr(), 2, self.D, self.layers[0].ln1[0].data_ptr(), self.layers[0].ln1[1].data_ptr(),
+                self.mel_pos.data_ptr(), 2, self.D, *self._embed_ln(),
                 st["x"].data_ptr(), st["h"].data_ptr(), _hip.dtype_code(st["h"]), st["B"],
                 _hip.ptr(st.get("forced")), _hip.stream_ptr()), "itts_sample_topk_embed")
             return
@@ -270,12 +310,64 @@ class HipGPT:
             st["logits"].data_ptr(), self.Vp, self.V, st["seen"].data_ptr(), st["done"].data_ptr(),
             st["codes"].data_ptr(), st["max_new"], st["t"].data_ptr(), col_delta, int(min_new), self.stop_mel,
             float(penalty), self.mel_emb.data_ptr(), self.mel_pos.data_ptr(), 2, self.D,
-            self.layers[0].ln1[0].data_ptr(), self.layers[0].ln1[1].data_ptr(), st["x"].data_ptr(),
+            *self._embed_ln(), st["x"].data_ptr(),
             st["h"].data_ptr(), _hip.dtype_code(st["h"]), st["B"], _hip.ptr(st.get("forced")), _hip.stream_ptr()),
             "itts_sample_embed")
 
+    def _dgx(self, A, wx, M, Y, epi=0, gelu=False, xh=None, nwaves=8):
+        """itts_decode_gemm16x: LayerNorm-folded store epilogue (wx["u"] set) or residual epilogue."""
+        _hip.check(self.lib.itts_decode_gemm16x(
+            A.data_ptr(), A.stride(0), wx["w16"].data_ptr(), wx["K"], wx["N"], M, _hip.ptr(wx["c"]),
+            _hip.ptr(wx["u"]), 1e-5, int(gelu), epi, Y.data_ptr(), Y.stride(0), _hip.dtype_code(Y), _hip.ptr(xh),
+            0 if xh is None else xh.stride(0), nwaves, _hip.stream_ptr()), "itts_decode_gemm16x")
+
+    def _decode_step_fold(self, st, min_new, penalty):
+        """bf16 product decode step, five launches per layer: c_attn (ln_1 folded) -> attention ->
+        attn.c_proj (x += ., x^ = bf16 x) -> c_fc (ln_2 folded, gelu) -> mlp.c_proj (split-K partials +
+        reduce, or full-K residual epilogue).  h holds x^ (the bf16 residual), never a LayerNorm output,
+        except after the last layer, whose reduce applies ln_f + final_norm (Q5) for mel_head."""
+        B, D = st["B"], self.D
+        stream = _hip.stream_ptr()
+        x, h, o, f = st["x"], st["h"], st["o"], st["f"]
+        qkv = st["qkv"][: B * 3 * D].view(B, 3 * D)
+        for li, ly in enumerate(self.layers):
+            self._dgx(h, ly.wx["qkv"], B, qkv)
+            kc, vc = st["kc"][li], st["vc"][li]
+            rows = st.get("kv_rows")
+            if rows is not None:
+                _hip.check(self.lib.itts_attn_decode_rows(
+                    qkv.data_ptr(), 3 * D, 1, B * 3 * D, None, kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+                    kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(), o.data_ptr(), D,
+                    B, self.H, _hip.dtype_code(kc), _hip.dtype_code(o), rows.data_ptr(), rows.stride(0), stream),
+                    "itts_attn_decode_rows")
+            else:
+                _hip.check(self.lib.itts_attn_decode(
+                    qkv.data_ptr(), 3 * D, 1, B * 3 * D, None, kc.data_ptr(), vc.data_ptr(), kc.stride(0),
+                    kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(), o.data_ptr(), D,
+                    B, self.H, _hip.dtype_code(kc), _hip.dtype_code(o), stream), "itts_attn_decode")
+            self._dgx(o, ly.wx["o"], B, x, epi=1, xh=h)
+            self._dgx(h, ly.wx["fc"], B, f, gelu=True)
+            last = li + 1 == self.L
+            if self.proj_fullk and not last:
+                self._dgx(f, ly.wx["proj"], B, x, epi=1, xh=h, nwaves=16)
+            else:
+                kp = self._ksplit(ly.w["proj"]["K"], self.KSPLIT["proj"])
+                self._dg(f, ly.w["proj"], B, None, st["ws"], epi=2, ksplit=kp)
+                if last:
+                    self._reduce(st, kp, ly.b["proj"], self.ln_f, self.final_norm)
+                else:
+                    self._reduce(st, kp, ly.b["proj"], (None, None))
+        self._dgw(h, self.head_w, B, self.head_b, st["logits"])
+        if "kv_rows" in st:
+            self._beam_step(st, 1)
+        else:
+            self._sample(st, 1, min_new, penalty)
+        _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
+
     def _decode_step(self, st, min_new, penalty):
         """One fed token per row -> next token sampled (all device-side; graph-capturable)."""
+        if self.fold:
+            return self._decode_step_fold(st, min_new, penalty)
         B, D = st["B"], self.D
         stream = _hip.stream_ptr()
         x, h, qkv, o, f = st["x"], st["h"], st["qkv"], st["o"], st["f"]
@@ -380,7 +472,7 @@ class HipGPT:
         x, h = st["x"], st["h"]
         _hip.check(self.lib.itts_residual_reduce_ln(
             x.data_ptr(), D, st["ws"].data_ptr(), nsplit, B * D, D, bias.data_ptr(), h.data_ptr(), D, B, D,
-            ln[0].data_ptr(), ln[1].data_ptr(), None if ln2 is None else ln2[0].data_ptr(),
+            _hip.ptr(ln[0]), _hip.ptr(ln[1]), None if ln2 is None else ln2[0].data_ptr(),
             None if ln2 is None else ln2[1].data_ptr(), _hip.dtype_code(h), _hip.stream_ptr()),
             "itts_residual_reduce_ln")
 
@@ -573,7 +665,7 @@ class HipGPT:
             float(smp[0]) if smp else 1.0, int(smp[1]) if smp else 0, float(smp[2]) if smp else 1.0, K,
             st["cand_key"].data_ptr(), st["cand_score"].data_ptr(), st["cand_tok"].data_ptr(), R, stream),
             "itts_beam_candidates")
-        ln1 = self.layers[0].ln1
+        ln1 = self._embed_ln()
         _hip.check(self.lib.itts_beam_select(
             st["cand_key"].data_ptr(), st["cand_score"].data_ptr(), st["cand_tok"].data_ptr(), K, self.V,
             self.stop_mel, int(smp is not None), float(bm["length_penalty"]), st["t"].data_ptr(), col_delta,
@@ -582,7 +674,7 @@ class HipGPT:
             st["kv_rows"].data_ptr(), st["kv_rows"].stride(0), st["s"] + 1, st["hyp_score"].data_ptr(),
             st["hyp_len"].data_ptr(), st["hyp_codes"].data_ptr(), st["hyp_n"].data_ptr(), st["hyp_order"].data_ptr(),
             st["hyp_worst"].data_ptr(), self.mel_emb.data_ptr(), self.mel_pos.data_ptr(), 2, self.D,
-            ln1[0].data_ptr(), ln1[1].data_ptr(), st["x"].data_ptr(), st["h"].data_ptr(), _hip.dtype_code(st["h"]),
+            ln1[0], ln1[1], st["x"].data_ptr(), st["h"].data_ptr(), _hip.dtype_code(st["h"]),
             R // K, st["max_new"], stream), "itts_beam_select")
 
     def _beam_state(self, B: int, K: int, max_new: int, s: int):

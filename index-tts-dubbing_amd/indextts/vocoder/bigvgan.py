@@ -169,10 +169,9 @@ class HipBigVGAN:
     # ---------------- per-prompt (cached by the caller) ----------------
     @torch.no_grad()
     def speaker(self, mel_ref: torch.Tensor) -> torch.Tensor:
-        """mel_ref [B, T, n_mels] -> [B, spk_dim] (ECAPA; PyTorch ops on the device).  MIOpen is
-        asked for deterministic conv algorithms: the default choice varies by ~4e-6 run to run."""
-        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
-            return speaker_embedding(self.sd_torch, mel_ref.to(self.device).float())
+        """mel_ref [B, T, n_mels] -> [B, spk_dim] (ECAPA; PyTorch ops on the device, convolutions as
+        im2col GEMMs: run-to-run identical without MIOpen's naive deterministic conv)."""
+        return speaker_embedding(self.sd_torch, mel_ref.to(self.device).float())
 
     @torch.no_grad()
     def cond_biases(self, spk: torch.Tensor):

@@ -1,7 +1,8 @@
 """ECAPA-TDNN speaker embedding applied to the prompt mel inside every vocoder call.
 
 Deterministic and per-prompt, so the host caches it (quirk Q6); PyTorch-ROCm code, not a
-hand-written kernel target.
+hand-written kernel target; convolutions as im2col GEMMs
+(``utils/convgemm.py``, §8(f) item 2).
 
 Reference behaviour followed:
   * ``ECAPA_TDNN.forward``                       BigVGAN/ECAPA_TDNN.py:543-581 (lengths=None)
@@ -18,6 +19,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..utils.convgemm import conv1d
+
 
 def _bn(x, sd, p):
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
@@ -30,7 +33,7 @@ def _conv_same(x, sd, p, dilation=1):
     pad = dilation * (k - 1) // 2
     if pad > 0:
         x = F.pad(x, (pad, pad), mode="reflect")
-    return F.conv1d(x, w, sd[p + ".bias"], dilation=dilation)
+    return conv1d(x, w, sd[p + ".bias"], dilation=dilation)
 
 
 def _tdnn(x, sd, p, dilation=1):

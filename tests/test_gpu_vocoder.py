@@ -78,7 +78,7 @@ def test_activation_kernel_bf16_paths_bit_equal_f32_path(C):
     lensd = lens.cuda()
     xb = x.cuda()
     xf = xb.float()
-    sentinel = -12345.0
+    sentinel = -12352.0  # exactly representable in bf16
     yb = torch.full((B, T, C), sentinel, dtype=torch.bfloat16, device="cuda")
     yf = torch.full((B, T, C), sentinel, dtype=torch.float32, device="cuda")
     for xin, yout, dt in ((xb, yb, _hip.BF16), (xf, yf, _hip.F32)):
