@@ -34,6 +34,10 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "audio-seconds/sec/GPU (RTF) IndexTTS-1.5 bf16 batch=32; 1→8 GPU scaling"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+# PMC traffic summaries of the CURRENT build (profiles/run_profiles.sh; FETCH_SIZE x2 per
+# MI355X_MICROARCH.md, calibrated by profiles/pmc_calibrate.py); None when not yet measured
+TRAFFIC_DECODE = "traffic_decode_r02.json"
+TRAFFIC_VOCODER = "traffic_vocoder_r02.json"
 
 
 class KernelTimer:
@@ -100,35 +104,77 @@ def make_inputs(cfg, indices, L, frames):
     return mels, texts
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_threads():
+    """threads for the CPU baseline: the cores this process may run on (sched affinity), capped by
+    OMP_NUM_THREADS when the launcher sets it (the GPU box gives one GPU's job a 16-CPU share while
+    os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    if os.environ.get("OMP_NUM_THREADS"):
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    return max(1, n)
+
+
 def cpu_baseline(cfg, gsd, vsd, B, N, L, frames):
-    """fp32 oracle (CPU restatement of the reference path) on a bounded sample: B utterances x N codes."""
+    """fp32 oracle (CPU restatement of the reference path, validated against the imported reference
+    by tests/test_oracle_golden.py) on bounded samples, per phase: C2 shape (1 utterance) and a C3-shape
+    sample (B utterances), N codes each (EOS suppressed).  ``value`` is the C3-shape sample's rate."""
     from indextts.gpt.conditioning import get_conditioning
     from indextts.vocoder.ecapa import speaker_embedding
     from oracle.bigvgan_oracle import BigVGANOracle, fold_weight_norm
     from oracle.gpt_oracle import GPTOracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     gt = {k: torch.from_numpy(np.asarray(v)) for k, v in gsd.items()}
     orc = GPTOracle(gt, cfg.gpt)
     voc = BigVGANOracle(vsd, cfg.bigvgan)
     vt = {k: v for k, v in fold_weight_norm(vsd).items()}
-    mels, texts = make_inputs(cfg, range(B), L, frames)
-    with torch.no_grad():
-        t0 = time.perf_counter()
-        mel = torch.cat(mels, 0)
-        conds = get_conditioning(gt, cfg.gpt, mel)
-        spk = speaker_embedding(vt, mel.transpose(1, 2))
-        codes = orc.generate(conds, torch.stack(texts), N, min_new_tokens=N)
-        audio = 0.0
-        for b in range(B):
-            fixed, _ = orc.remove_long_silence(codes[b:b + 1])
-            lat = orc.latent(conds[b:b + 1], texts[b][None], fixed)
-            wav = voc.forward(lat, spk[b:b + 1])
-            audio += wav.shape[-1] / 24000.0
-        dt = time.perf_counter() - t0
-    return {"value": round(audio / dt, 4), "unit": "audio-seconds/sec", "cores": threads, "kind": "port",
-            "sample": f"{B} utterances x {N} codes (L={L}, {frames}-frame prompts), fp32 oracle incl. conditioning, "
-                      f"ECAPA, greedy decode, latent pass and vocoder; {audio:.2f} audio-s in {dt:.1f} s"}
+
+    def run(nb):
+        mels, texts = make_inputs(cfg, range(nb), L, frames)
+        ph = {}
+        with torch.no_grad():
+            t = time.perf_counter()
+            mel = torch.cat(mels, 0)
+            conds = get_conditioning(gt, cfg.gpt, mel)
+            spk = speaker_embedding(vt, mel.transpose(1, 2))
+            ph["conditioning_ecapa"] = time.perf_counter() - t
+            t = time.perf_counter()
+            codes = orc.generate(conds, torch.stack(texts), N, min_new_tokens=N)
+            ph["decode"] = time.perf_counter() - t
+            lat_t = voc_t = 0.0
+            audio = 0.0
+            for b in range(nb):
+                t = time.perf_counter()
+                fixed, _ = orc.remove_long_silence(codes[b:b + 1])
+                lat = orc.latent(conds[b:b + 1], texts[b][None], fixed)
+                lat_t += time.perf_counter() - t
+                t = time.perf_counter()
+                wav = voc.forward(lat, spk[b:b + 1])
+                voc_t += time.perf_counter() - t
+                audio += wav.shape[-1] / 24000.0
+            ph["latent"], ph["vocoder"] = lat_t, voc_t
+        tot = sum(ph.values())
+        return audio, tot, {k: round(v, 3) for k, v in ph.items()}
+
+    a2, t2, ph2 = run(1)
+    a3, t3, ph3 = run(B)
+    return {"value": round(a3 / t3, 4), "unit": "audio-seconds/sec", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "visible_cpus": os.cpu_count(),
+            "sample": f"C3-shape sample: {B} utterances x {N} codes (L={L}, {frames}-frame prompts, EOS suppressed), "
+                      f"fp32 oracle incl. conditioning, ECAPA, greedy decode, latent pass and vocoder; {a3:.2f} "
+                      f"audio-s in {t3:.1f} s on {threads} threads",
+            "phases_s": ph3, "c2": {"value": round(a2 / t2, 4), "sample": f"1 utterance x {N} codes", "phases_s": ph2}}
 
 
 def main():
@@ -150,6 +196,10 @@ def main():
                          "utterance), c5 (srt_dubbing long-form: a synthetic SRT of --cues cues sharded over the "
                          "ranks, length-bucketed chunks of 32 streamed through the pipelined driver)")
     ap.add_argument("--cues", type=int, default=256)
+    ap.add_argument("--decoding", choices=("greedy", "beam3"), default="greedy",
+                    help="greedy (the headline) or beam3: the reference's default production decoding "
+                         "(do_sample=True, num_beams=3, top_k=30, top_p=0.8, infer.py:535-543), 3 beam rows "
+                         "per utterance (96-row decode step at batch 32)")
     ap.add_argument("--pipeline", action="store_true",
                     help="run the K timed batches through BatchedTTS.synthesize_many (decode of batch i+1 "
                          "overlapped with the latent pass + vocoder of batch i)")
@@ -191,8 +241,12 @@ def main():
     mels = [m.to(dev) for m in mels]
     texts = [t.to(dev) for t in texts]
 
+    dec_kw = {}
+    if args.decoding == "beam3":
+        dec_kw = dict(do_sample=True, num_beams=3, top_k=30, top_p=0.8, temperature=1.0, seed=1234)
+
     def step():
-        pcm, lens, _ = tts.synthesize(mels, texts, max_mel_tokens=N, min_new_tokens=N)
+        pcm, lens, _ = tts.synthesize(mels, texts, max_mel_tokens=N, min_new_tokens=N, **dec_kw)
         if world > 1:  # the one collective: finished int16 waveforms to rank 0, in utterance order
             gather_waveforms([pcm[b, : int(lens[b])] for b in range(B)], B * world, dev)
         return float(lens.sum()) / SR
@@ -209,7 +263,7 @@ def main():
     t0 = time.perf_counter()
     audio = 0.0
     if args.pipeline:
-        res = tts.synthesize_many([(mels, texts)] * args.steps, max_mel_tokens=N, min_new_tokens=N)
+        res = tts.synthesize_many([(mels, texts)] * args.steps, max_mel_tokens=N, min_new_tokens=N, **dec_kw)
         torch.cuda.synchronize()
         for pcm, lens, _ in res:
             if world > 1:
@@ -230,8 +284,11 @@ def main():
         d_ms = sum(a.elapsed_time(b) for a, b, _, _ in step_ev)
         d_bytes = sum(tts.gpt.step_weight_bytes + keys * tts.gpt.kv_bytes_per_key for _, _, _, keys in step_ev)
         gbs = d_bytes / (d_ms * 1e-3) / 1e9
-        dec = {"kernel": "GPT decode step (hipGraph: 20 x [c_attn GEMM, attention, c_proj GEMM (split-K 8), reduce+LN, "
-                         "c_fc GEMM (16-column tiles), mlp.c_proj GEMM, reduce+LN] + mel_head GEMM + sampler)", "bound": "hbm",
+        rows = step_ev[0][2]
+        dec = {"kernel": f"GPT decode step, {rows} rows (hipGraph: 20 x [c_attn GEMM (ln_1 folded), attention, "
+                         "attn.c_proj GEMM (residual epilogue), c_fc GEMM (ln_2 folded, gelu), mlp.c_proj GEMM "
+                         "(split-K 8), reduce] + mel_head GEMM + " + ("beam candidates/select)" if args.decoding == "beam3"
+                                                                       else "sampler)"), "bound": "hbm",
                "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
                "traffic": None, "launches": len(step_ev), "avg_launch_us": round(1e3 * d_ms / len(step_ev), 2),
                "algorithmic_bytes_per_launch": round(d_bytes / len(step_ev)), "share_of_step": round(d_ms / (1e3 * dt), 3)}
@@ -249,12 +306,12 @@ def main():
     voc = {"kernel": "itts_igemm_fwd (BigVGAN convs C >= 192 and ConvTranspose phases, MFMA bf16)", "bound": "mfma",
            "achieved": None if achieved is None else round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
            "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / PEAK_BF16_TFLOPS, 4),
-           "traffic": _traffic("traffic_vocoder_r01.json", "igemm_bytes_per_launch"), "launches": k_n,
+           "traffic": _traffic(TRAFFIC_VOCODER, "igemm_bytes_per_launch"), "launches": k_n,
            "avg_launch_us": round(1e3 * k_ms / max(k_n, 1), 2),
            "algorithmic_bytes_per_launch": round(timer.bytes / max(k_n, 1)),
            "share_of_step": round(k_ms / (1e3 * dt), 3)}
-    if dec is not None:  # the decode step is the dominant unit of work (>60 % of the step)
-        dec["traffic"] = _traffic("traffic_decode_r01.json", "bytes_per_step")
+    if dec is not None and args.decoding == "greedy":  # the decode step: the dominant unit of work
+        dec["traffic"] = _traffic(TRAFFIC_DECODE, "bytes_per_step")
     cpu = None
     if args.breakdown:
         ph = {}
@@ -267,6 +324,8 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic: seeded random-init IndexTTS-1.5 weights, random 511-frame prompt mels, random text ids",
+        "per_gpu_value": round(audio / dt / world, 3),
+        "decoding": "greedy" if args.decoding == "greedy" else "beam sample, num_beams=3, top_k=30, top_p=0.8",
         "config": {"workload": f"{'C2' if args.workload == 'c2' else 'C3'}: batch={B} zero-shot utterance"
                                f"{'s' if B > 1 else ''} per GPU (one prompt each), L={L} text ids, "
                                f"{N} codes each (EOS suppressed): conditioning+ECAPA, GPT prefill+decode (hipGraph), "
@@ -284,9 +343,10 @@ def main():
 def long_form(args, cfg, gsd, vsd, dev, world, rank):
     """C5 (BASELINE.json configs[4]): srt_dubbing long-form.  A synthetic SRT of args.cues cues (seed 3),
     cue text L ~ U[8, 96], one shared prompt (features computed once, cached by key); cue i runs on rank
-    i % world; each rank sorts its cues by length into chunks of 32 (texts padded to the chunk's bucket
-    with the stop id 1, which prepare_gpt_inputs strips: per-cue results are unchanged), 6 codes per
-    text token of the bucket (EOS suppressed), and streams the chunks through the pipelined driver;
+    i % world; each rank sorts its cues by length into chunks of 32 (the decode ids padded to the chunk's
+    bucket with the stop id 1 via ``pad_to`` -- prepare_gpt_inputs strips it, the latent pass gets the
+    unpadded ids: per-cue results are unchanged), 6 codes per text token of the bucket (EOS
+    suppressed), and streams the chunks through the pipelined driver;
     the finished waveforms are gathered to rank 0.  One step = the whole SRT."""
     from indextts.pipeline import BatchedTTS, SR
     from indextts.sharding import gather_waveforms, shard
@@ -304,8 +364,8 @@ def long_form(args, cfg, gsd, vsd, dev, world, rank):
         idx = mine[c: c + 32]
         order += idx
         bl = next(b for b in buckets if b >= max(int(lens_all[i]) for i in idx))
-        tx = [torch.cat([texts_all[i], torch.ones(bl - len(texts_all[i]), dtype=torch.int64)]).to(dev) for i in idx]
-        batches.append(([mel] * len(idx), tx, {"max_mel_tokens": 6 * bl, "min_new_tokens": 6 * bl}))
+        tx = [texts_all[i].to(dev) for i in idx]
+        batches.append(([mel] * len(idx), tx, {"max_mel_tokens": 6 * bl, "min_new_tokens": 6 * bl, "pad_to": bl}))
         keys.append([("prompt", 0)] * len(idx))
 
     def step():

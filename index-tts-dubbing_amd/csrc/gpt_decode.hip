@@ -82,8 +82,10 @@ __device__ __forceinline__ void ln_vec(float (&v)[KPL], const float* g, const fl
 // EPI: 0 store act(acc + bias) as OutT; 1 f32 Y += acc + bias; 2 split-K over gridDim.y, each split
 // stores its f32 partial product (an in-kernel last-arriver reduction was measured slower: the two
 // agent-scope fences it needs cost more than the separate reduce launch).
-template <int NW, int LNMODE, int EPI, int KLN, typename OutT>
+// MT (LNMODE 0 only): 32-row tiles per workgroup sharing every weight fragment (beam decoding).
+template <int NW, int LNMODE, int EPI, int KLN, typename OutT, int MT = 1>
 __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
+  static_assert(MT == 1 || LNMODE == 0, "row-tile batching needs a bf16 A operand");
   constexpr int APITCH = KLN * 2 + 16;  // LDS row pitch (bytes) of the normalised A tile
   constexpr int RED_BYTES = NW * 16 * 64 * sizeof(float);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -139,23 +141,29 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
     __syncthreads();
   }
 
-  f32x16_t acc;
+  f32x16_t acc[MT];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  auto afrag = [&](int s) -> bf16x8_t {
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  auto afrag = [&](int s, int t) -> bf16x8_t {
     if (LNMODE) return *reinterpret_cast<const bf16x8_t*>(As + r32 * APITCH + 32 * s + 16 * h);
     const uint16_t* A = reinterpret_cast<const uint16_t*>(p.a);
-    return *reinterpret_cast<const bf16x8_t*>(A + (int64_t)r32 * p.lda + 16 * s + 8 * h);
+    return *reinterpret_cast<const bf16x8_t*>(A + (int64_t)(32 * t + r32) * p.lda + 16 * s + 8 * h);
   };
   auto compute = [&](const u32x4_t (&src)[kU], int i0) {
-    bf16x8_t af[kU] = {};
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (i0 + u < niter) af[u] = afrag(kbeg + w + NW * (i0 + u));
+    for (int t = 0; t < MT; ++t) {
+      bf16x8_t af[kU] = {};
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (i0 + u < niter)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[u], *reinterpret_cast<const bf16x8_t*>(&src[u]), acc, 0, 0, 0);
+      for (int u = 0; u < kU; ++u)
+        if (i0 + u < niter) af[u] = afrag(kbeg + w + NW * (i0 + u), t);
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (i0 + u < niter)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[u], *reinterpret_cast<const bf16x8_t*>(&src[u]), acc[t],
+                                                           0, 0, 0);
+    }
   };
   for (int i0 = 0; i0 < niter; i0 += 2 * kU) {
     if (i0 + kU < niter) wload(wb, i0 + kU);
@@ -164,45 +172,72 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
     if (i0 + kU < niter) compute(wb, i0 + kU);
   }
 
+  // epilogue tile by tile through one [NW][16][64] LDS buffer (32 KiB at NW = 8, any MT)
   float* myred = red + w * 16 * 64;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) myred[r * 64 + lane] = acc[r];
-  __syncthreads();
   constexpr int PER = 1024 / (64 * NW);  // tile outputs per thread
-  float tv[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int o = threadIdx.x + 64 * NW * k;
-    float v = 0.f;
+  for (int tile = 0; tile < MT; ++tile) {
+    if (tile > 0) __syncthreads();  // previous tile's reads done
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) v += red[ww * 1024 + o];
-    tv[k] = v;
-  }
+    for (int r = 0; r < 16; ++r) myred[r * 64 + lane] = acc[tile][r];
+    __syncthreads();
+    float tv[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int o = threadIdx.x + 64 * NW * k;
-    const int r = o / 64, l = o % 64;
-    const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-    const int n = nt * 32 + (l & 31);
-    if (row >= p.M || n >= p.N) continue;
-    if (EPI == 2) {  // split-K partial (no bias); reduced in fixed order by itts_residual_reduce_ln
-      reinterpret_cast<float*>(p.y)[ks * p.split_stride + (int64_t)row * p.ldy + n] = tv[k];
-      continue;
+    for (int k = 0; k < PER; ++k) {
+      const int o = threadIdx.x + 64 * NW * k;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += red[ww * 1024 + o];
+      tv[k] = v;
     }
-    float v = tv[k];
-    if (p.bias) v += p.bias[n];
-    if (EPI >= 1) {
-      float* Y = reinterpret_cast<float*>(p.y) + (int64_t)row * p.ldy + n;
-      *Y = *Y + v;
-    } else {
-      if (p.gelu) v = gelu_tanh_d(v);
-      St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int o = threadIdx.x + 64 * NW * k;
+      const int r = o / 64, l = o % 64;
+      const int row = 32 * tile + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      const int n = nt * 32 + (l & 31);
+      if (row >= p.M || n >= p.N) continue;
+      if (EPI == 2) {  // split-K partial (no bias); reduced in fixed order by itts_residual_reduce_ln
+        reinterpret_cast<float*>(p.y)[ks * p.split_stride + (int64_t)row * p.ldy + n] = tv[k];
+        continue;
+      }
+      float v = tv[k];
+      if (p.bias) v += p.bias[n];
+      if (EPI >= 1) {
+        float* Y = reinterpret_cast<float*>(p.y) + (int64_t)row * p.ldy + n;
+        *Y = *Y + v;
+      } else {
+        if (p.gelu) v = gelu_tanh_d(v);
+        St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
+      }
     }
   }
 }
 
 template <int NW, int LNMODE, int EPI, int KLN, typename OutT>
 void launch_dg(const DgArgs& a, int row_tiles, int ksplit, hipStream_t s) {
+  if constexpr (LNMODE == 0) {
+    if (row_tiles > 1) {  // up to 4 row tiles per launch share the weight stream
+      for (int t = 0; t < row_tiles; t += 4) {
+        DgArgs b = a;
+        const int64_t ra = (int64_t)t * 32;
+        const int rows = a.M - 32 * t < 128 ? a.M - 32 * t : 128, mt = (rows + 31) / 32;
+        b.M = rows;
+        b.a = reinterpret_cast<const uint16_t*>(a.a) + ra * a.lda;
+        if (EPI >= 1) b.y = reinterpret_cast<float*>(a.y) + ra * a.ldy;
+        else b.y = reinterpret_cast<OutT*>(a.y) + ra * a.ldy;
+        const dim3 grid((a.N + 31) / 32, ksplit), block(64 * NW);
+        const size_t lds = NW * 16 * 64 * sizeof(float);
+        switch (mt) {
+          case 1: hipLaunchKernelGGL((decode_gemm_kernel<NW, 0, EPI, KLN, OutT, 1>), grid, block, lds, s, b); break;
+          case 2: hipLaunchKernelGGL((decode_gemm_kernel<NW, 0, EPI, KLN, OutT, 2>), grid, block, lds, s, b); break;
+          case 3: hipLaunchKernelGGL((decode_gemm_kernel<NW, 0, EPI, KLN, OutT, 3>), grid, block, lds, s, b); break;
+          default: hipLaunchKernelGGL((decode_gemm_kernel<NW, 0, EPI, KLN, OutT, 4>), grid, block, lds, s, b); break;
+        }
+      }
+      return;
+    }
+  }
   size_t lds = NW * 16 * 64 * sizeof(float) + (LNMODE ? 32 * (KLN * 2 + 16) : 0);
   for (int t = 0; t < row_tiles; ++t) {
     DgArgs b = a;
@@ -328,11 +363,14 @@ struct Dg16xArgs {
   int64_t ldxh;
 };
 
-template <int NW, bool FOLD, int EPI, typename OutT>
+// MT = 32-row tiles per workgroup (beam decoding: 3 x 32 rows): every weight fragment is loaded once
+// and multiplied into all MT tiles, so the weights cross HBM once per step, not once per tile.
+template <int NW, bool FOLD, int EPI, typename OutT, int MT>
 __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
-  __shared__ float red[NW][8][64];
-  __shared__ float rsum[FOLD ? NW : 1][32], rsq[FOLD ? NW : 1][32];
-  __shared__ float mu[32], rs[32];
+  constexpr int R = 32 * MT;
+  __shared__ float red[NW][8][64];  // one 32-row tile at a time
+  __shared__ float rsum[FOLD ? NW : 1][FOLD ? R : 1], rsq[FOLD ? NW : 1][FOLD ? R : 1];
+  __shared__ float mu[FOLD ? R : 1], rs[FOLD ? R : 1];
   const int nt = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ksteps = p.K / 32;
@@ -348,34 +386,35 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
       if (i0 + u < niter) dst[u] = __builtin_nontemporal_load(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
   };
   wload(wa, 0);
-  f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;  // FOLD: row c16 / 16 + c16 sums over this lane's A
+  f32x4_t acc[2 * MT];
+  float ssum[2 * MT], ssq[2 * MT];  // FOLD: sums of the rows this lane holds (16-row half h: c16 + 16h)
+#pragma unroll
+  for (int t = 0; t < 2 * MT; ++t) {
+    acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    ssum[t] = ssq[t] = 0.f;
+  }
   auto compute = [&](const u32x4_t (&src)[kU], int i0) {
-    bf16x8_t a0[kU] = {}, a1[kU] = {};
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (i0 + u < niter) {
-        const int64_t col = 32 * (w + NW * (i0 + u)) + 8 * q;
-        a0[u] = *reinterpret_cast<const bf16x8_t*>(A + (int64_t)c16 * p.lda + col);
-        a1[u] = *reinterpret_cast<const bf16x8_t*>(A + (int64_t)(16 + c16) * p.lda + col);
-      }
+    for (int u = 0; u < kU; ++u) {
+      if (i0 + u >= niter) continue;
+      const int64_t col = 32 * (w + NW * (i0 + u)) + 8 * q;
+      bf16x8_t av[2 * MT];
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (i0 + u < niter) {
-        const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&src[u]);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bfr, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bfr, acc1, 0, 0, 0);
+      for (int t = 0; t < 2 * MT; ++t) av[t] = *reinterpret_cast<const bf16x8_t*>(A + (int64_t)(16 * t + c16) * p.lda + col);
+      const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&src[u]);
+#pragma unroll
+      for (int t = 0; t < 2 * MT; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[t], bfr, acc[t], 0, 0, 0);
         if constexpr (FOLD) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float v0 = (float)a0[u][e], v1 = (float)a1[u][e];
-            s0 += v0;
-            q0 = fmaf(v0, v0, q0);
-            s1 += v1;
-            q1 = fmaf(v1, v1, q1);
+            const float v = (float)av[t][e];
+            ssum[t] += v;
+            ssq[t] = fmaf(v, v, ssq[t]);
           }
         }
       }
+    }
   };
   for (int i0 = 0; i0 < niter; i0 += 2 * kU) {
     if (i0 + kU < niter) wload(wb, i0 + kU);
@@ -383,70 +422,75 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
     if (i0 + 2 * kU < niter) wload(wa, i0 + 2 * kU);
     if (i0 + kU < niter) compute(wb, i0 + kU);
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    red[w][r][lane] = acc0[r];
-    red[w][4 + r][lane] = acc1[r];
-  }
   if constexpr (FOLD) {
-    s0 += __shfl_xor(s0, 16, 64);
-    s0 += __shfl_xor(s0, 32, 64);
-    q0 += __shfl_xor(q0, 16, 64);
-    q0 += __shfl_xor(q0, 32, 64);
-    s1 += __shfl_xor(s1, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    q1 += __shfl_xor(q1, 16, 64);
-    q1 += __shfl_xor(q1, 32, 64);
-    if (q == 0) {
-      rsum[w][c16] = s0;
-      rsq[w][c16] = q0;
-      rsum[w][16 + c16] = s1;
-      rsq[w][16 + c16] = q1;
+#pragma unroll
+    for (int t = 0; t < 2 * MT; ++t) {
+      float a = ssum[t], b = ssq[t];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (q == 0) {
+        rsum[w][16 * t + c16] = a;
+        rsq[w][16 * t + c16] = b;
+      }
     }
   }
-  __syncthreads();
   if constexpr (FOLD) {
-    if (threadIdx.x < 32) {
+    __syncthreads();
+    for (int r = threadIdx.x; r < R; r += 64 * NW) {
       float S = 0.f, Q = 0.f;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) {
-        S += rsum[ww][threadIdx.x];
-        Q += rsq[ww][threadIdx.x];
+        S += rsum[ww][r];
+        Q += rsq[ww][r];
       }
       const float inv = 1.0f / p.K, m = S * inv;
-      mu[threadIdx.x] = m;
-      rs[threadIdx.x] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
+      mu[r] = m;
+      rs[r] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
     }
     __syncthreads();
   }
-  // 512 outputs (32 rows x 16 columns); C/D layout of 16x16x32: row = 4*(lane>>4) + reg, col = lane&15
-  for (int o = threadIdx.x; o < 512; o += 64 * NW) {
-    const int e = o >> 6, l = o & 63;  // e = 4 * (row half) + reg
-    float v = 0.f;
+  // R rows x 16 columns, one 32-row tile at a time through red; C/D layout of 16x16x32:
+  // row = 4*(lane>>4) + reg, col = lane&15
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) v += red[ww][e][l];
-    const int row = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
-    const int n = nt * 16 + (l & 15);
-    if (row >= p.M || n >= p.N) continue;
-    if constexpr (FOLD) v = rs[row] * (v - mu[row] * p.u[n]);
-    if (p.c) v += p.c[n];
-    if constexpr (EPI == 1) {
-      float* X = reinterpret_cast<float*>(p.y) + (int64_t)row * p.ldy + n;
-      const float xv = *X + v;
-      *X = xv;
-      p.xh[(int64_t)row * p.ldxh + n] = f2bf(xv);
-    } else {
-      if (p.gelu) v = gelu_tanh_d(v);
-      St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
+  for (int tile = 0; tile < MT; ++tile) {
+    if (tile > 0) __syncthreads();  // previous tile's reads done
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w][4 * hf + r][lane] = acc[2 * tile + hf][r];
+    __syncthreads();
+    for (int o = threadIdx.x; o < 512; o += 64 * NW) {
+      const int e = o >> 6, l = o & 63;  // e = 4 * (16-row half) + reg
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += red[ww][e][l];
+      const int row = 32 * tile + 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
+      const int n = nt * 16 + (l & 15);
+      if (row >= p.M || n >= p.N) continue;
+      if constexpr (FOLD) v = rs[row] * (v - mu[row] * p.u[n]);
+      if (p.c) v += p.c[n];
+      if constexpr (EPI == 1) {
+        float* X = reinterpret_cast<float*>(p.y) + (int64_t)row * p.ldy + n;
+        const float xv = *X + v;
+        *X = xv;
+        p.xh[(int64_t)row * p.ldxh + n] = f2bf(xv);
+      } else {
+        if (p.gelu) v = gelu_tanh_d(v);
+        St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
+      }
     }
   }
 }
 
 template <int NW, bool FOLD, int EPI, typename OutT>
 void launch_dg16x(const Dg16xArgs& a, hipStream_t s) {
-  for (int t = 0; t * 32 < a.M; ++t) {
+  // up to 4 row tiles (128 rows) per launch share the weight stream; more rows: further launches
+  for (int t = 0; t * 32 < a.M; t += 4) {
     Dg16xArgs b = a;
-    b.M = a.M - 32 * t < 32 ? a.M - 32 * t : 32;
+    const int rows = a.M - 32 * t < 128 ? a.M - 32 * t : 128;
+    b.M = rows;
     b.a = a.a + (int64_t)t * 32 * a.lda;
     if (EPI == 1) {
       b.y = reinterpret_cast<float*>(a.y) + (int64_t)t * 32 * a.ldy;
@@ -454,7 +498,13 @@ void launch_dg16x(const Dg16xArgs& a, hipStream_t s) {
     } else {
       b.y = reinterpret_cast<OutT*>(a.y) + (int64_t)t * 32 * a.ldy;
     }
-    hipLaunchKernelGGL((decode_gemm16x_kernel<NW, FOLD, EPI, OutT>), dim3((a.N + 15) / 16), dim3(64 * NW), 0, s, b);
+    const dim3 grid((a.N + 15) / 16), block(64 * NW);
+    switch ((rows + 31) / 32) {
+      case 1: hipLaunchKernelGGL((decode_gemm16x_kernel<NW, FOLD, EPI, OutT, 1>), grid, block, 0, s, b); break;
+      case 2: hipLaunchKernelGGL((decode_gemm16x_kernel<NW, FOLD, EPI, OutT, 2>), grid, block, 0, s, b); break;
+      case 3: hipLaunchKernelGGL((decode_gemm16x_kernel<NW, FOLD, EPI, OutT, 3>), grid, block, 0, s, b); break;
+      default: hipLaunchKernelGGL((decode_gemm16x_kernel<NW, FOLD, EPI, OutT, 4>), grid, block, 0, s, b); break;
+    }
   }
 }
 
@@ -535,7 +585,8 @@ extern "C" int itts_decode_gemm16(const void* a, int64_t lda, const void* w_pack
 //   else:             y = a @ W^T + c
 //   epi 0: store act(y) as out_dtype (act = gelu_tanh if gelu)
 //   epi 1: residual, y is the f32 stream x [M][ldy]: x += y in place, xh[M][ldxh] = bf16(x)
-// nwaves: 8 or 16 waves per workgroup.
+// nwaves: 8 or 16 waves per workgroup.  A holds whole 32-row tiles (rows >= M are read, never stored);
+// up to 128 rows share one weight stream.
 extern "C" int itts_decode_gemm16x(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M,
                                    const float* c, const float* u, float eps, int gelu, int epi, void* y, int64_t ldy,
                                    int out_dtype, void* xh, int64_t ldxh, int nwaves, void* stream) {

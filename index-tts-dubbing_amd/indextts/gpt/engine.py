@@ -767,11 +767,22 @@ class HipGPT:
         if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
             ln["graph"] = (self._capture(st, min_new_tokens, repetition_penalty), gkey)
         steps = 1
+        ev = self.step_events  # optional instrumentation (bench.py): HIP events around each step
+        # distinct cache keys a step reads: each utterance's prompt once (shared by its beams through
+        # the lineage table) + every beam row's generated keys
+        keys0 = int(B * (s + 1) - int(pad.sum())) if ev is not None else 0
         while steps < max_new_tokens:
+            if ev is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             if graph_ok:
                 ln["graph"][0].replay()
             else:
                 self._decode_step(st, min_new_tokens, repetition_penalty)
+            if ev is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                ev.append((e0, e1, R, keys0 + R * steps))
             steps += 1
             if steps % check_every == 0 and bool(st["done_u"].all()):
                 break

@@ -119,11 +119,15 @@ class BatchedTTS:
     @torch.no_grad()
     def synthesize(self, mels: Sequence[torch.Tensor], texts: Sequence[torch.Tensor], max_mel_tokens: int = 600,
                    repetition_penalty: float = 10.0, min_new_tokens: int = 0, keys=None, use_graph: bool = True,
-                   timings: Optional[dict] = None, vocoder_groups: Optional[List[List[int]]] = None, **sampling):
+                   timings: Optional[dict] = None, vocoder_groups: Optional[List[List[int]]] = None,
+                   pad_to: int = 0, **sampling):
         """mels[b]: prompt log-mel [1, 100, T_b]; texts[b]: token ids [L_b].
         -> (pcm int16 [B, Tmax] on device, sample lengths [B] (cpu), codes list).
         ``timings``: if a dict is given, per-phase wall seconds are accumulated into it (adds syncs).
         ``sampling``: do_sample / temperature / top_k / top_p / seed (HipGPT.generate).
+        ``pad_to``: pad the text ids for ``generate`` to at least this length (with the stop id, which
+        prepare_gpt_inputs strips -- per-utterance ids unchanged) so that batches of a length bucket share
+        one captured decode graph; the latent pass always gets the unpadded ids.
         ``vocoder_groups``: utterance index lists whose latents are concatenated along time before the
         vocoder (``infer_fast`` decodes pairs of sentences as one latent, infer.py:440-458); the pcm /
         lengths then have one row per group (speaker embedding of the group's first member)."""
@@ -142,7 +146,7 @@ class BatchedTTS:
         B = len(texts)
         conds, spk = self.prompt_features(mels, keys)
         mark("prompt_features")
-        L = max(int(t.numel()) for t in texts)
+        L = max([int(t.numel()) for t in texts] + [int(pad_to)])
         ids = torch.full((B, L), self.stop_text, dtype=torch.long)
         for b, t in enumerate(texts):
             ids[b, : t.numel()] = t.reshape(-1).long()
@@ -166,7 +170,7 @@ class BatchedTTS:
     def synthesize_many(self, batches: Sequence[tuple], max_mel_tokens: int = 600, repetition_penalty: float = 10.0,
                         min_new_tokens: int = 0, keys=None, front_priority: int = -1, streams=None, **sampling):
         """Pipelined ``synthesize`` over several batches [(mels, texts[, {"max_mel_tokens": n,
-        "min_new_tokens": m}]), ...]: the front half (prompt
+        "min_new_tokens": m, "pad_to": L}]), ...] (``pad_to`` as in ``synthesize``): the front half (prompt
         features, GPT decode, remove_long_silence) of batch i+1 runs on a high-priority stream while
         the back half (latent pass + vocoder) of batch i runs on a second stream.  The decode step is a
         latency-bound chain of small kernels that leaves most CUs idle; the vocoder's MFMA/HBM-heavy
@@ -190,7 +194,7 @@ class BatchedTTS:
             B = len(texts)
             with torch.cuda.stream(front):
                 conds, spk = self.prompt_features(mels, None if keys is None else keys[bi])
-                L = max(int(t.numel()) for t in texts)
+                L = max([int(t.numel()) for t in texts] + [int(over.get("pad_to", 0))])
                 ids = torch.full((B, L), self.stop_text, dtype=torch.long)
                 for b, t in enumerate(texts):
                     ids[b, : t.numel()] = t.reshape(-1).long()

@@ -6,7 +6,7 @@
 # Large traces stay under /tmp on the box; only the small summaries come back.
 set -e
 export TMPDIR=/tmp
-TAG=${1:-r01}
+TAG=${1:-r02}
 mkdir -p gpurun_out
 rm -rf /tmp/prof /tmp/pmc_*
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof -o run -- \
@@ -20,5 +20,7 @@ if [ "${2:-pmc}" = "pmc" ]; then
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pmc_vf -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vf.log 2>&1
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pmc_vw -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vw.log 2>&1
   python3 profiles/traffic.py vocoder /tmp/pmc_vf /tmp/pmc_vw > gpurun_out/traffic_vocoder_$TAG.json
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pmc_c -o run -- python3 profiles/pmc_calibrate.py > gpurun_out/pmc_c.log 2>&1
+  python3 profiles/traffic.py calibrate /tmp/pmc_c > gpurun_out/traffic_calibration_$TAG.json
 fi
 echo profiles-done

@@ -7,6 +7,9 @@ wide coalesced streaming reads, so it is doubled; WRITE_SIZE is exact for 16-B-p
 usage:
   python profiles/traffic.py vocoder <fetch_dir> <write_dir>
       igemm_kernel dispatches of the second of two vocoder forwards (profiles/pmc_vocoder.py)
+  python profiles/traffic.py calibrate <fetch_dir>
+      measured FETCH_SIZE of the known-byte c_fc GEMM dispatches (profiles/pmc_calibrate.py) / their
+      weight bytes: ~0.5 confirms the x2 correction for this access pattern
   python profiles/traffic.py decode <fetch_dir> <write_dir>
       the GPT decode-step kernels (profiles/pmc_decode.py), summed per step; one step = one
       advance_kernel dispatch; dispatches before the first attn_decode_kernel (prefill) skipped
@@ -18,8 +21,8 @@ import json
 import os
 import sys
 
-DECODE_KERNELS = ("attn_decode_kernel", "decode_gemm_kernel", "residual_reduce_ln", "sample_embed_kernel",
-                  "sample_topk_embed_kernel", "advance_kernel")
+DECODE_KERNELS = ("attn_decode_kernel", "decode_gemm_kernel", "decode_gemm16_kernel", "decode_gemm16x_kernel",
+                  "residual_reduce_ln", "sample_embed_kernel", "sample_topk_embed_kernel", "advance_kernel")
 
 
 def load(d, counter):
@@ -36,7 +39,7 @@ def load(d, counter):
 
 
 def short(name):
-    for k in DECODE_KERNELS + ("igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel"):
+    for k in sorted(DECODE_KERNELS, key=len, reverse=True) + ["igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel"]:
         if k in name:
             return k
     return name.split("(")[0][-40:]
@@ -77,7 +80,21 @@ def decode(fetch, write):
             "correction": "FETCH_SIZE x2 (gfx950 coalesced-read undercount); KiB -> bytes"}
 
 
+def calibrate(fetch):
+    weight_bytes = 4096 * 1024 * 2
+    ids = sorted(k for k, (n, _) in fetch.items() if "decode_gemm16x_kernel" in n)
+    raw = [1024 * fetch[k][1] for k in ids[2:]]  # skip the first (cold code / TLB) dispatches
+    mean = sum(raw) / len(raw)
+    return {"kernel": "decode_gemm16x_kernel, N=4096 K=1024 M=32 (c_fc shape), distinct weight copies",
+            "dispatches": len(raw), "weight_bytes": weight_bytes, "fetch_size_bytes_per_dispatch": mean,
+            "ratio_fetch_size_to_weight_bytes": mean / weight_bytes,
+            "note": "ratio ~0.5 = FETCH_SIZE counts half the bytes of 16-B-per-lane streaming reads (x2 correction)"}
+
+
 def main():
+    if sys.argv[1] == "calibrate":
+        print(json.dumps(calibrate(load(sys.argv[2], "FETCH_SIZE")), indent=1))
+        return
     mode, fdir, wdir = sys.argv[1:4]
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
     print(json.dumps(vocoder(fetch, write) if mode == "vocoder" else decode(fetch, write), indent=1))

@@ -16,7 +16,7 @@ def _lib():
 
 
 @pytest.mark.parametrize("K,N,M", [(256, 96, 3), (256, 256, 1), (512, 512, 1), (1024, 3072, 32), (1024, 8194, 32),
-                                   (4096, 1024, 32), (1024, 1024, 45)])
+                                   (4096, 1024, 32), (1024, 1024, 45), (1024, 1024, 96), (4096, 1024, 150)])
 @pytest.mark.parametrize("mode", ["plain", "ln", "ln2", "resid", "split2", "split8", "gelu_bf16"])
 def test_decode_gemm(K, N, M, mode):
     from indextts.gpt.engine import pack_skinny
@@ -107,6 +107,72 @@ def test_decode_gemm16(K, N, M, gelu):
     tol = (2e-2 if gelu else 1e-2) * scale + (1e-2 if gelu else 0)
     err = (got - ref).abs()
     assert bool((err <= tol).all()), float((err / scale).max())
+    if Mp > M:
+        assert torch.equal(Y[M:].float().cpu(), Y0[M:].to(Y.dtype).float())
+
+
+@pytest.mark.parametrize("K,N,M", [(1024, 3072, 32), (1024, 4096, 45), (1024, 1024, 96), (4096, 1024, 32),
+                                   (512, 96, 3), (1024, 3072, 160)])
+@pytest.mark.parametrize("mode", ["fold", "fold_gelu_bf16", "plain", "resid"])
+def test_decode_gemm16x(K, N, M, mode):
+    """itts_decode_gemm16x vs torch fp32 on the same bf16 operands.
+    fold: y = LN(a) @ W + bias computed as rstd * (a @ W' - mean * u) + c (W' = bf16(diag(g) W),
+    row statistics of the bf16 rows of a): compared with exactly that expression in fp32 (|err| <=
+    1e-2 * rstd * (|a| @ |W'|)) AND with the unfolded LN(a) @ W + bias within the bf16 weight
+    rounding (2e-2 relative to the same scale); resid: x += a @ W^T + bias in place and
+    xh = bf16(x); rows >= M untouched; M > 32 exercises the row-tile batching (weights read once)."""
+    from indextts.gpt.engine import fold_ln_weights
+    _hip, lib = _lib()
+    torch.manual_seed(K * 7 + N + M)
+    Mp = (M + 31) // 32 * 32
+    W_io = torch.randn(K, N) / K ** 0.5  # HF Conv1D [in, out]
+    bias = torch.randn(N) * 0.1
+    g, b = torch.randn(K) * 0.1 + 1, torch.randn(K) * 0.1
+    fold = mode.startswith("fold")
+    wx = fold_ln_weights(W_io, bias, (g, b) if fold else None, "cuda")
+    X = torch.randn(Mp, K) * 1.5 + 0.3
+    A = X.to(torch.bfloat16).float()
+    gelu = mode == "fold_gelu_bf16"
+    out_bf16 = gelu
+    if fold:
+        Wp = (W_io * g[:, None]).to(torch.bfloat16).float()  # W' [K, N]
+        mu = A[:M].mean(1, keepdim=True)
+        var = (A[:M] ** 2).mean(1, keepdim=True) - mu ** 2
+        rstd = torch.rsqrt(var + 1e-5)
+        ref = rstd * (A[:M] @ Wp - mu * Wp.sum(0)) + (b @ W_io + bias)
+        scale = rstd * (A[:M].abs() @ Wp.abs()) + 1e-3
+        unfolded = F.layer_norm(A[:M], (K,), g, b, 1e-5) @ W_io + bias
+    else:
+        Wq = W_io.to(torch.bfloat16).float()
+        ref = A[:M] @ Wq + bias
+        scale = A[:M].abs() @ Wq.abs() + 1e-3
+    if gelu:
+        ref = F.gelu(ref, approximate="tanh")
+    Y0 = torch.randn(Mp, N)
+    xh0 = torch.randn(Mp, N).to(torch.bfloat16)
+    if mode == "resid":
+        ref = ref + Y0[:M]
+        Y = Y0.clone().cuda()
+        xh = xh0.clone().cuda()
+    else:
+        Y = Y0.clone().to(torch.bfloat16 if out_bf16 else torch.float32).cuda()
+        xh = None
+    a_dev = X.to(torch.bfloat16).cuda()
+    _hip.check(lib.itts_decode_gemm16x(a_dev.data_ptr(), K, wx["w16"].data_ptr(), K, N, M, _hip.ptr(wx["c"]),
+                                       _hip.ptr(wx["u"]), 1e-5, int(gelu), int(mode == "resid"), Y.data_ptr(), N,
+                                       _hip.dtype_code(Y), _hip.ptr(xh), N, 8, _hip.stream_ptr()), "gemm16x")
+    torch.cuda.synchronize()
+    got = Y[:M].float().cpu()
+    assert torch.isfinite(got).all()
+    tol = 1e-2 * scale + (1e-2 if out_bf16 else 0)
+    err = (got - ref).abs()
+    assert bool((err <= tol).all()), float((err / scale).max())
+    if fold and not gelu:
+        assert bool(((got - unfolded).abs() <= 2e-2 * scale + 1e-3).all())
+    if mode == "resid":
+        assert torch.equal(xh[:M].cpu(), Y[:M].cpu().to(torch.bfloat16))
+        if Mp > M:
+            assert torch.equal(xh[M:].cpu(), xh0[M:])
     if Mp > M:
         assert torch.equal(Y[M:].float().cpu(), Y0[M:].to(Y.dtype).float())
 
