@@ -8,7 +8,7 @@
  *     legacy default stream); launches are asynchronous, no host synchronisation;
  *   - return 0 on success, nonzero on an argument error or a HIP launch error; the message is in
  *     itts_last_error() (thread-local); no C++ exception crosses the ABI;
- *   - dtype codes: ITTS_F32 = 0, ITTS_BF16 = 1;
+ *   - dtype codes: ITTS_F32 = 0, ITTS_BF16 = 1, ITTS_F16 = 2 (f16: the activation op only);
  *   - "channel-last" vocoder activations are [B][T][C] with per-sequence lengths[B] (ragged batch):
  *     rows t >= lengths[b] are never read as data (edge handling equals the reference's padding);
  *   - callable from any host thread; ctypes releases the GIL around every call.
@@ -27,12 +27,15 @@
 extern "C" {
 #endif
 
-enum { ITTS_DTYPE_F32 = 0, ITTS_DTYPE_BF16 = 1 };
+enum { ITTS_DTYPE_F32 = 0, ITTS_DTYPE_BF16 = 1, ITTS_DTYPE_F16 = 2 };
 
 /* ---- runtime -------------------------------------------------------------------------------- */
 const char* itts_last_error(void);
 int itts_abi_version(void);
 const char* itts_build_target(void); /* "gfx950" */
+/* sizeof of the ABI structs below (0 ItTsGptLayerW, 1 ItTsGptWeights, 2 ItTsGptDecodeState,
+ * 3 ItTsSampling), -1 otherwise: lets a binding check its struct layouts. */
+int64_t itts_struct_size(int which);
 
 /* ---- BigVGAN2 vocoder ----------------------------------------------------------------------- */
 
@@ -42,7 +45,9 @@ const char* itts_build_target(void); /* "gfx950" */
  * (anti_alias_activation_cuda.cu:214-256) and its torch path Activation1d.forward
  * (alias_free_torch/act.py:24-29, resample.py:25-49, filter.py:87-96, activations.py:109-122);
  * the parity target is the torch path (quirk Q7: the CUDA kernel differs on the first/last 3 samples).
- * Arbitrary strides (x_sb/x_st/x_sc = batch/time/channel strides); lengths may be NULL (all T). */
+ * Arbitrary strides (x_sb/x_st/x_sc = batch/time/channel strides); lengths may be NULL (all T).
+ * dtypes: f32 / bf16 in any in-out combination, or f16 -> f16 (the reference op's float / bf16 / half
+ * dispatch, type_shim.h:20-43); the arithmetic is f32 throughout, outputs rounded to nearest even. */
 int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, const float* down12, const float* log_alpha,
                           const float* log_beta, const int32_t* lengths, int B, int C, int T, int64_t x_sb,
                           int64_t x_st, int64_t x_sc, int64_t y_sb, int64_t y_st, int64_t y_sc, int dtype_in,
@@ -128,7 +133,7 @@ int itts_decode_gemm16(const void* a, int64_t lda, const void* w_packed16, int K
  * (HF ln_1 -> c_attn / ln_2 -> c_fc, modeling_gpt2.py:246-306).  With u == NULL: y = a @ W^T + c.
  * epi 0: store act(y) (gelu_tanh if gelu) as out_dtype; epi 1 (attn.c_proj / mlp.c_proj): residual,
  * y is the f32 stream x[M][ldy]: x += y, and xh[M][ldxh] = bf16(x) (the next A operand).
- * nwaves = 8 or 16 per workgroup. */
+ * nwaves = 4, 8 or 16 per workgroup. */
 int itts_decode_gemm16x(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M, const float* c,
                         const float* u, float eps, int gelu, int epi, void* y, int64_t ldy, int out_dtype, void* xh,
                         int64_t ldxh, int nwaves, void* stream);
@@ -212,6 +217,106 @@ int itts_beam_select(const float* cand_key, const float* cand_score, const int32
                      void* stream);
 /* tstate[0] += delta on the device (advances the decode column between graph replays). */
 int itts_step_advance(int32_t* tstate, int delta, void* stream);
+
+/* ---- fused decode launches and the whole decode step (bf16 product mode, rows <= 128) ---------- */
+
+/* c_attn (ln_1 folded, as itts_decode_gemm16x with u/c) AND the attention of itts_attn_decode[_rows]
+ * in ONE launch: producer blocks store q/k/v (f32 [R][ldqkv], write-through) and count per head into
+ * counters[H] (zeroed by the caller before the launch); attention blocks request their cached K/V
+ * first, then wait for their head.  Results equal itts_decode_gemm16x + itts_attn_decode bit for bit.
+ * timeout: one word set (never cleared by the library) if a wait gave up.
+ * HF modeling_gpt2.py:246-306 (ln_1, c_attn), :54-72 and :185-225 (attention, cache update). */
+int itts_decode_qkv_attn(const void* xh, int64_t ldxh, const void* w_packed16, const float* u, const float* c,
+                         float eps, float* qkv, int64_t ldqkv, void* cache_k, void* cache_v, int64_t cache_bs,
+                         int64_t cache_hs, int smax, const int32_t* pad, int kv_base, const int32_t* tstate, void* out,
+                         int64_t ldo, int R, int H, const int32_t* kv_rows, int64_t ld_rows, uint32_t* counters,
+                         uint32_t* timeout, void* stream);
+/* c_fc (ln_2 folded, gelu) + mlp.c_proj (split-K, ksplit = 8) + the residual reduce in ONE launch:
+ * x += proj_b + sum_s partial_s (split order) and xh = bf16(x), equal bit for bit to
+ * itts_decode_gemm16x + itts_decode_gemm(epi 2) + itts_residual_reduce_ln (no LayerNorm).
+ * counters: [ksplit] group counters then [D/32] column-tile tickets, zeroed before the launch.
+ * HF modeling_gpt2.py:229-243 (MLP) and :246-306 (ln_2, residual). */
+int itts_decode_mlp(const void* xh, int64_t ldxh, const void* fc_w16, const float* fc_u, const float* fc_c, float eps,
+                    void* f, int64_t ldf, const void* proj_w, const float* proj_b, float* part, float* x,
+                    int64_t ldx, int R, int D, int ksplit, uint32_t* counters, uint32_t* timeout, void* stream);
+
+/* Weights of one GPT-2 block in the decode packings (engine.fold_ln_weights / pack_skinny[16]). */
+typedef struct ItTsGptLayerW {
+  const void* qkv_w16;  /* diag(ln_1.g) W_c_attn, 16-column fragment order */
+  const float* qkv_u;   /* column sums of qkv_w16 */
+  const float* qkv_c;   /* ln_1.b^T W_c_attn + c_attn.bias */
+  const void* o_w16;    /* attn.c_proj, 16-column fragment order */
+  const float* o_c;     /* attn.c_proj.bias */
+  const void* fc_w16;   /* diag(ln_2.g) W_c_fc, 16-column fragment order */
+  const float* fc_u;
+  const float* fc_c;
+  const void* proj_w;   /* mlp.c_proj, 32-column fragment order */
+  const float* proj_b;
+} ItTsGptLayerW;
+
+/* The UnifiedVoice GPT for decoding (gpt/model.py:255-281,85-192): layers, ln_f + final_norm (Q5),
+ * mel_head, the mel embeddings fed back (Q1 positions). */
+typedef struct ItTsGptWeights {
+  int n_layer, d_model, n_head;
+  int n_mel_codes, logits_pitch;  /* V = 8194; row pitch of logits / seen (>= V, multiple of 4) */
+  int start_mel, stop_mel;
+  const ItTsGptLayerW* layers;    /* HOST array [n_layer] */
+  const float *ln_f_g, *ln_f_b, *final_g, *final_b;
+  const void* head_w;             /* mel_head, 32-column fragment order */
+  const float* head_b;
+  const float* mel_emb;           /* [V][D] f32 */
+  const float* mel_pos;           /* [max positions][D] f32 */
+} ItTsGptWeights;
+
+/* Device-resident decode state of `rows` sequences (the caller allocates everything). */
+typedef struct ItTsGptDecodeState {
+  int rows, max_kv, kv_base, max_new;  /* kv_base = prompt length s + 1; step j writes key kv_base + j */
+  float* x;          /* residual stream [rows][D] f32 */
+  void* xh;          /* its bf16 copy, [32-row padded][D] */
+  float* qkv;        /* [rows][3D] f32 */
+  void* o;           /* attention output [32-row padded][D] bf16 */
+  void* f;           /* gelu(c_fc) [32-row padded][4D] bf16 */
+  float* part;       /* split-K partials [8][rows][D] f32 */
+  float* logits;     /* [rows][logits_pitch] f32 */
+  void* k_cache;     /* [n_layer][rows][n_head][max_kv][64] bf16 */
+  void* v_cache;
+  const int32_t* pad;      /* [rows] left padding (Q2) */
+  int32_t* tstate;         /* [4]: step, row base, RNG seed lo / hi */
+  const int32_t* kv_rows;  /* beams: [rows][ld_rows] KV lineage table, else NULL */
+  int64_t ld_rows;
+  uint8_t* seen;           /* [rows][logits_pitch] repetition-penalty flags */
+  uint8_t* done;           /* [rows] */
+  int32_t* codes;          /* [rows][max_new] */
+  const int32_t* forced;   /* teacher forcing (tests) or NULL */
+  void* workspace;         /* itts_gpt_decode_workspace_bytes(); last 16 B: timeout word (zero it once) */
+  int launch_mode;         /* 0: one kernel per phase; 1: the two multi-role launches per layer
+                              (itts_decode_qkv_attn, itts_decode_mlp); 2: as 0, plus each layer's
+                              K/V read ahead on a side stream (forked after the previous layer's
+                              attention, joined before this one's) into the Infinity Cache */
+} ItTsGptDecodeState;
+
+/* Token selection of the step: mode 0 greedy (itts_sample_embed), 1 top-k / top-p sampling
+ * (itts_sample_topk_embed), 2 logits only (beam search: the caller runs itts_beam_candidates /
+ * itts_beam_select and itts_step_advance). */
+typedef struct ItTsSampling {
+  int mode, min_new;
+  float rep_penalty, temperature;
+  int top_k;
+  float top_p;
+} ItTsSampling;
+
+/* Bytes of ItTsGptDecodeState.workspace (hand-off counters + the timeout word), or -1. */
+int64_t itts_gpt_decode_workspace_bytes(const ItTsGptWeights* w);
+/* One whole KV-cached decode step (one HF generate iteration of inference_speech, gpt/model.py:655-708).
+ * launch_mode 0, per layer: c_attn with ln_1 folded (itts_decode_gemm16x) -> itts_attn_decode[_rows] ->
+ * attn.c_proj (itts_decode_gemm16x residual) -> c_fc with ln_2 folded + gelu -> mlp.c_proj split-K 8
+ * (itts_decode_gemm) -> itts_residual_reduce_ln (the last layer's with ln_f + final_norm, Q5).
+ * launch_mode 1, per layer: itts_decode_qkv_attn -> attn.c_proj -> itts_decode_mlp (last layer as in
+ * mode 0), one memset node zeroing the hand-off counters first.  Then mel_head, token selection + next
+ * embedding (modes 0/1 of ItTsSampling) and the step advance.  Graph-capturable: the step counter
+ * lives on the device. */
+int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecodeState* state, const ItTsSampling* sampling,
+                         void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,8 @@
 // One workgroup = 256 threads = a [TT x CT] (time x channel) output tile; the raw input window
 // [TT+12 x CT] is staged once through LDS as f32 (replicate-clamped rows), then each thread runs a
 // 16-output register window along time for one channel (HBM-bound: 1 read + 1 write per element).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -177,7 +179,7 @@ void launch(const ActArgs& a, bool vec, bool vout, hipStream_t s) {
   dim3 grid((a.T + a.nsub * kTO - 1) / (a.nsub * kTO), (a.C + a.CT - 1) / a.CT, a.B);
   const int TT = a.nsub * kTO;
   size_t lds = sizeof(float) * (size_t)(TT + 2 * kHalo) * a.CT;
-  if constexpr (sizeof(TO) == 2) {
+  if constexpr (std::is_same<TO, uint16_t>::value) {
     if (vout) {
       lds += sizeof(uint16_t) * (size_t)TT * a.CT;
       if (vec)
@@ -203,8 +205,10 @@ extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, 
   ITTS_REQUIRE(B >= 0 && C >= 0 && T >= 0, fn, "negative size");
   if (B == 0 || C == 0 || T == 0) return 0;
   ITTS_REQUIRE(x && y && up12 && down12 && log_alpha && log_beta, fn, "null pointer");
-  ITTS_REQUIRE((dtype_in == ITTS_F32 || dtype_in == ITTS_BF16) && (dtype_out == ITTS_F32 || dtype_out == ITTS_BF16),
-               fn, "unsupported dtype (f32=0, bf16=1)");
+  ITTS_REQUIRE((dtype_in == ITTS_F32 || dtype_in == ITTS_BF16 || dtype_in == ITTS_F16) &&
+                   (dtype_out == ITTS_F32 || dtype_out == ITTS_BF16 || dtype_out == ITTS_F16),
+               fn, "unsupported dtype (f32=0, bf16=1, f16=2)");
+  ITTS_REQUIRE((dtype_in == ITTS_F16) == (dtype_out == ITTS_F16), fn, "f16 input needs f16 output (and vice versa)");
   ActArgs a{x, y, up12, down12, log_alpha, log_beta, lengths, B, C, T, 0, 0, x_sb, x_st, x_sc, y_sb, y_st, y_sc};
   // channel tile: all channels when C <= 64, else 64 -- or 32 when 32 divides C and 64 does not
   // (C = 96: two 64-channel tiles would leave half the second tile's threads idle)
@@ -217,7 +221,8 @@ extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, 
   // vectorised output through LDS: channel-last bf16 output, 16-B aligned rows
   const bool vout = dtype_out == ITTS_BF16 && y_sc == 1 && C % 8 == 0 && y_st % 8 == 0 && y_sb % 8 == 0 &&
                     (reinterpret_cast<uintptr_t>(y) & 15) == 0;
-  if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, vout, s);
+  if (dtype_in == ITTS_F16) launch<_Float16, _Float16>(a, false, false, s);  // f32 math, RNE half stores
+  else if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, vout, s);
   else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, false, false, s);
   else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, false, vout, s);
   else launch<uint16_t, float>(a, vec, false, s);

@@ -13,7 +13,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
 
-enum ItTsDtype { ITTS_F32 = 0, ITTS_BF16 = 1 };
+enum ItTsDtype { ITTS_F32 = 0, ITTS_BF16 = 1, ITTS_F16 = 2 };
 
 // ---- bf16 <-> f32 (bf16 carried as raw uint16_t) ----
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
@@ -34,6 +34,11 @@ template <> struct St<uint16_t> {
   __device__ __forceinline__ static float ld(const uint16_t* p) { return bf2f(*p); }
   __device__ __forceinline__ static void st(uint16_t* p, float v) { *p = f2bf(v); }
 };
+// IEEE half (the reference activation op also dispatches Half: type_shim.h:20-43); round to nearest even
+template <> struct St<_Float16> {
+  __device__ __forceinline__ static float ld(const _Float16* p) { return (float)*p; }
+  __device__ __forceinline__ static void st(_Float16* p, float v) { *p = (_Float16)v; }
+};
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -43,6 +48,22 @@ __device__ __forceinline__ float wave_sum(float v) {
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Sum over each aligned group of 8 lanes, every lane of the group receiving the same value: DPP
+// quad_perm xor-1 and xor-2 (within 4 lanes) then row_half_mirror (lane i <-> 7 - i of each 8),
+// all VALU data-path operands -- no LDS round trip as ds_swizzle / ds_bpermute would take
+// (attention at S = 283: 13.6 -> 12.7 us).  Each step adds the same two values in every lane
+// (a + b == b + a), so the 8 lanes agree bitwise.
+template <int CTRL>
+__device__ __forceinline__ float mov_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8_dpp(float v) {
+  v += mov_dpp<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v += mov_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v += mov_dpp<0x141>(v);  // row_half_mirror: lanes 0-3 <-> 7-4
   return v;
 }
 

@@ -36,22 +36,6 @@ __device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]
   }
 }
 
-// Sum over each aligned group of 8 lanes, every lane of the group receiving the same value: DPP
-// quad_perm xor-1 and xor-2 (within 4 lanes) then row_half_mirror (lane i <-> 7 - i of each 8),
-// all VALU data-path operands -- no LDS round trip as ds_swizzle / ds_bpermute would take
-// (attention at S = 283: 13.6 -> 12.7 us).  Each step adds the same two values in every lane
-// (a + b == b + a), so the 8 lanes agree bitwise.
-template <int CTRL>
-__device__ __forceinline__ float mov_dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float sum8_dpp(float v) {
-  v += mov_dpp<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
-  v += mov_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
-  v += mov_dpp<0x141>(v);  // row_half_mirror: lanes 0-3 <-> 7-4
-  return v;
-}
-
 constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is the caller's
 
 // One workgroup of NT threads per (head, sequence): NT/8 groups of 8 lanes, group g owns keys

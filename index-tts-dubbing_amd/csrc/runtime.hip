@@ -29,3 +29,15 @@ extern "C" int itts_abi_version(void) { return 1; }
 
 // Which gfx target this code object was built for (sanity check from the host).
 extern "C" const char* itts_build_target(void) { return "gfx950"; }
+
+// sizeof of the ABI structs (include/itts_hip.h), so bindings can check their layouts:
+// 0 ItTsGptLayerW, 1 ItTsGptWeights, 2 ItTsGptDecodeState, 3 ItTsSampling
+extern "C" int64_t itts_struct_size(int which) {
+  switch (which) {
+    case 0: return sizeof(ItTsGptLayerW);
+    case 1: return sizeof(ItTsGptWeights);
+    case 2: return sizeof(ItTsGptDecodeState);
+    case 3: return sizeof(ItTsSampling);
+    default: return -1;
+  }
+}

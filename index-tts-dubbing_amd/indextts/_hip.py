@@ -18,7 +18,7 @@ LIB_NAME = "libitts_hip.so"
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG_DIR, LIB_NAME)
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 
 _c_i = ctypes.c_int
 _c_i64 = ctypes.c_int64
@@ -31,6 +31,7 @@ SIGNATURES = {
     "itts_last_error": (ctypes.c_char_p, []),
     "itts_abi_version": (_c_i, []),
     "itts_build_target": (ctypes.c_char_p, []),
+    "itts_struct_size": (_c_i64, [_c_i]),
     "itts_aa_snakebeta_fwd": (_c_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_i64, _c_i64, _c_i64,
                                      _c_i64, _c_i64, _c_i64, _c_i, _c_i, _vp]),
     "itts_aa_snakebeta_bct": (_c_i, [_vp, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_i, _vp]),
@@ -70,7 +71,39 @@ SIGNATURES = {
     "itts_step_advance": (_c_i, [_vp, _c_i, _vp]),
     "itts_decode_gemm": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _vp,
                                 _c_i64, _c_i, _c_i64, _c_i, _vp]),
+    "itts_decode_qkv_attn": (_c_i, [_vp, _c_i64, _vp, _vp, _vp, _c_f, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_i, _vp,
+                                    _c_i, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _c_i64, _vp, _vp, _vp]),
+    "itts_decode_mlp": (_c_i, [_vp, _c_i64, _vp, _vp, _vp, _c_f, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_i, _c_i,
+                               _c_i, _vp, _vp, _vp]),
+    "itts_gpt_decode_workspace_bytes": (_c_i64, [_vp]),
+    "itts_gpt_decode_step": (_c_i, [_vp, _vp, _vp, _vp]),
 }
+
+
+# ---- structs of the whole-step entry point (include/itts_hip.h; field order is the ABI) ----------
+class GptLayerW(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("qkv_w16", "qkv_u", "qkv_c", "o_w16", "o_c", "fc_w16", "fc_u", "fc_c",
+                                   "proj_w", "proj_b")]
+
+
+class GptWeights(ctypes.Structure):
+    _fields_ = [("n_layer", _c_i), ("d_model", _c_i), ("n_head", _c_i), ("n_mel_codes", _c_i),
+                ("logits_pitch", _c_i), ("start_mel", _c_i), ("stop_mel", _c_i),
+                ("layers", ctypes.POINTER(GptLayerW))] + \
+        [(n, _vp) for n in ("ln_f_g", "ln_f_b", "final_g", "final_b", "head_w", "head_b", "mel_emb", "mel_pos")]
+
+
+class GptDecodeState(ctypes.Structure):
+    _fields_ = [("rows", _c_i), ("max_kv", _c_i), ("kv_base", _c_i), ("max_new", _c_i)] + \
+        [(n, _vp) for n in ("x", "xh", "qkv", "o", "f", "part", "logits", "k_cache", "v_cache", "pad", "tstate",
+                            "kv_rows")] + \
+        [("ld_rows", _c_i64)] + [(n, _vp) for n in ("seen", "done", "codes", "forced", "workspace")] + \
+        [("launch_mode", _c_i)]
+
+
+class Sampling(ctypes.Structure):
+    _fields_ = [("mode", _c_i), ("min_new", _c_i), ("rep_penalty", _c_f), ("temperature", _c_f), ("top_k", _c_i),
+                ("top_p", _c_f)]
 
 _lib = None
 _lock = threading.Lock()
@@ -125,6 +158,8 @@ def dtype_code(t) -> int:
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype == torch.float16:
+        return F16
     raise HipError(f"unsupported dtype {t.dtype}")
 
 

@@ -15,6 +15,7 @@ done flags, codes) lives on the device so one captured hipGraph replays every st
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from typing import List, Optional
@@ -116,6 +117,15 @@ class HipGPT:
         #  * mlp.c_proj: split-K 8 + reduce launch (default) or one full-K launch of 64 workgroups with
         #    the residual epilogue (ITTS_PROJ_FULLK=1)
         self.proj_fullk = self.fold and os.environ.get("ITTS_PROJ_FULLK", "0") == "1"
+        #  * the whole step as ONE C-ABI call, itts_gpt_decode_step (gpt_step.hip), replaying the same
+        #    launches as _decode_step_fold (ITTS_CSTEP=0: the Python launch sequence); ITTS_MULTIROLE=1:
+        #    its multi-role launches (c_attn + attention, c_fc + mlp.c_proj + reduce in one launch each,
+        #    in-launch hand-offs) -- bit-identical, measured SLOWER (profiles/ubench_fused_r02.txt)
+        self.cstep = self.fold and os.environ.get("ITTS_CSTEP", "1") != "0"
+        self.multirole = self.cstep and os.environ.get("ITTS_MULTIROLE", "0") == "1"
+        self.qkv_nwaves = 8  # c_attn waves per workgroup (the multi-role launch's producers run 4)
+        #  * ITTS_KV_PREFETCH=1: each layer's K/V read ahead into the Infinity Cache on a side stream
+        self.kv_prefetch = self.cstep and os.environ.get("ITTS_KV_PREFETCH", "0") == "1"
         self.layers: List[_Layer] = []
         for i in range(self.L):
             p = f"gpt.h.{i}"
@@ -140,6 +150,8 @@ class HipGPT:
             self.layers.append(ly)
         self.head_w = self._pack(sd["mel_head.weight"].float().contiguous(), igemm=False)
         self.head_b = f32("mel_head.bias")
+        if self.fold:
+            self._cweights = self._c_weights()
         self._lanes = {}  # lane index -> decode state, captured graph, stream
         self.step_events = None  # set to a list to time every decode step with HIP events (bench.py)
         self.logits_trace = None  # set to a list to record every step's raw logits [B, V] (tests)
@@ -321,6 +333,65 @@ class HipGPT:
             _hip.ptr(wx["u"]), 1e-5, int(gelu), epi, Y.data_ptr(), Y.stride(0), _hip.dtype_code(Y), _hip.ptr(xh),
             0 if xh is None else xh.stride(0), nwaves, _hip.stream_ptr()), "itts_decode_gemm16x")
 
+    def _c_weights(self):
+        """ItTsGptWeights (include/itts_hip.h) over this engine's packed tensors (kept alive by self)."""
+        L = len(self.layers)
+        arr = (_hip.GptLayerW * L)()
+        for i, ly in enumerate(self.layers):
+            wx = ly.wx
+            arr[i] = _hip.GptLayerW(wx["qkv"]["w16"].data_ptr(), wx["qkv"]["u"].data_ptr(), wx["qkv"]["c"].data_ptr(),
+                                    wx["o"]["w16"].data_ptr(), wx["o"]["c"].data_ptr(), wx["fc"]["w16"].data_ptr(),
+                                    wx["fc"]["u"].data_ptr(), wx["fc"]["c"].data_ptr(), ly.w["proj"]["sk"].data_ptr(),
+                                    ly.b["proj"].data_ptr())
+        w = _hip.GptWeights(L, self.D, self.H, self.V, self.Vp, self.start_mel, self.stop_mel, arr,
+                            self.ln_f[0].data_ptr(), self.ln_f[1].data_ptr(), self.final_norm[0].data_ptr(),
+                            self.final_norm[1].data_ptr(), self.head_w["sk"].data_ptr(), self.head_b.data_ptr(),
+                            self.mel_emb.data_ptr(), self.mel_pos.data_ptr())
+        w._layers = arr  # keep the array alive with the struct
+        return w
+
+    def _c_state(self, st):
+        """ItTsGptDecodeState over one decode state's tensors (rebuilt per call: `forced` may change)."""
+        if "sync" not in st:
+            nb = int(self.lib.itts_gpt_decode_workspace_bytes(ctypes.byref(self._cweights)))
+            st["sync"] = torch.zeros((nb + 3) // 4, dtype=torch.int32, device=self.dev)
+        kv_rows = st.get("kv_rows")
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        return _hip.GptDecodeState(
+            st["B"], self.max_kv, st["s"] + 1, st["max_new"], p(st["x"]), p(st["h"]), p(st["qkv"]), p(st["o"]),
+            p(st["f"]), p(st["ws"]), p(st["logits"]), p(st["kc"]), p(st["vc"]), p(st["pad"]), p(st["t"]), p(kv_rows),
+            0 if kv_rows is None else kv_rows.stride(0), p(st["seen"]), p(st["done"]), p(st["codes"]),
+            p(st.get("forced")), p(st["sync"]), 1 if self.multirole else (2 if self.kv_prefetch else 0))
+
+    def decode_timed_out(self, st) -> bool:
+        """True if a hand-off wait of the multi-role launches gave up (the step's results are invalid)."""
+        return "sync" in st and bool(st["sync"][-4:].any())
+
+    def _check_timeout(self, st):
+        if self.decode_timed_out(st):
+            st["sync"].zero_()
+            raise _hip.HipError("itts_gpt_decode_step: a hand-off wait timed out (results invalid)")
+
+    def _decode_step_c(self, st, min_new, penalty):
+        """bf16 product decode step as ONE C-ABI call (itts_gpt_decode_step, gpt_step.hip): the launches
+        of _decode_step_fold (or the multi-role launches), mel_head, token selection, step advance.
+        Bit-identical to _decode_step_fold (tests/test_gpu_fused.py)."""
+        beams = "kv_rows" in st
+        smp = st.get("sampling")
+        if beams:
+            mode = _hip.Sampling(2, 0, 1.0, 1.0, 0, 1.0)
+        elif smp is None:
+            mode = _hip.Sampling(0, int(min_new), float(penalty), 1.0, 0, 1.0)
+        else:
+            mode = _hip.Sampling(1, int(min_new), float(penalty), float(smp[0]), int(smp[1]), float(smp[2]))
+        cst = self._c_state(st)
+        stream = _hip.stream_ptr()
+        _hip.check(self.lib.itts_gpt_decode_step(ctypes.byref(self._cweights), ctypes.byref(cst), ctypes.byref(mode),
+                                                 stream), "itts_gpt_decode_step")
+        if beams:
+            self._beam_step(st, 1)
+            _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
+
     def _decode_step_fold(self, st, min_new, penalty):
         """bf16 product decode step, five launches per layer: c_attn (ln_1 folded) -> attention ->
         attn.c_proj (x += ., x^ = bf16 x) -> c_fc (ln_2 folded, gelu) -> mlp.c_proj (split-K partials +
@@ -331,7 +402,7 @@ class HipGPT:
         x, h, o, f = st["x"], st["h"], st["o"], st["f"]
         qkv = st["qkv"][: B * 3 * D].view(B, 3 * D)
         for li, ly in enumerate(self.layers):
-            self._dgx(h, ly.wx["qkv"], B, qkv)
+            self._dgx(h, ly.wx["qkv"], B, qkv, nwaves=self.qkv_nwaves)
             kc, vc = st["kc"][li], st["vc"][li]
             rows = st.get("kv_rows")
             if rows is not None:
@@ -366,6 +437,8 @@ class HipGPT:
 
     def _decode_step(self, st, min_new, penalty):
         """One fed token per row -> next token sampled (all device-side; graph-capturable)."""
+        if self.cstep and (st["B"] <= 128 or not self.multirole):
+            return self._decode_step_c(st, min_new, penalty)
         if self.fold:
             return self._decode_step_fold(st, min_new, penalty)
         B, D = st["B"], self.D
@@ -533,7 +606,8 @@ class HipGPT:
         sampling = (float(temperature), int(top_k), float(top_p)) if do_sample else None
         if do_sample and seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None)
+        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None, self.cstep, self.multirole,
+                self.qkv_nwaves, self.kv_prefetch)
         main = torch.cuda.current_stream(self.dev)
         work = []
         for i, (r0, r1) in enumerate(self._lane_bounds(B, lanes)):
@@ -577,6 +651,7 @@ class HipGPT:
                     break
         for ln in work:
             main.wait_stream(ln["stream"])
+            self._check_timeout(ln["st"])
         codes = torch.cat([ln["st"]["codes"][:, :steps] for ln in work], 0).long()
         hit = codes == self.stop_mel
         if bool(hit.any(dim=1).all()):
@@ -762,7 +837,8 @@ class HipGPT:
         else:
             self._dgw(st["h"], self.head_w, R, self.head_b, st["logits"])
         self._beam_step(st, 0)
-        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling)
+        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep, self.multirole,
+                self.qkv_nwaves, self.kv_prefetch)
         graph_ok = use_graph and max_new_tokens > 1
         if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
             ln["graph"] = (self._capture(st, min_new_tokens, repetition_penalty), gkey)
@@ -786,6 +862,7 @@ class HipGPT:
             steps += 1
             if steps % check_every == 0 and bool(st["done_u"].all()):
                 break
+        self._check_timeout(st)
         return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
 
     def _beam_finalize(self, st, B, K, steps, max_new, length_penalty):
