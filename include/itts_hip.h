@@ -133,7 +133,7 @@ int itts_decode_gemm16(const void* a, int64_t lda, const void* w_packed16, int K
  * (HF ln_1 -> c_attn / ln_2 -> c_fc, modeling_gpt2.py:246-306).  With u == NULL: y = a @ W^T + c.
  * epi 0: store act(y) (gelu_tanh if gelu) as out_dtype; epi 1 (attn.c_proj / mlp.c_proj): residual,
  * y is the f32 stream x[M][ldy]: x += y, and xh[M][ldxh] = bf16(x) (the next A operand).
- * nwaves = 4, 8 or 16 per workgroup. */
+ * nwaves = 8 or 16 per workgroup. */
 int itts_decode_gemm16x(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M, const float* c,
                         const float* u, float eps, int gelu, int epi, void* y, int64_t ldy, int out_dtype, void* xh,
                         int64_t ldxh, int nwaves, void* stream);
@@ -218,27 +218,7 @@ int itts_beam_select(const float* cand_key, const float* cand_score, const int32
 /* tstate[0] += delta on the device (advances the decode column between graph replays). */
 int itts_step_advance(int32_t* tstate, int delta, void* stream);
 
-/* ---- fused decode launches and the whole decode step (bf16 product mode, rows <= 128) ---------- */
-
-/* c_attn (ln_1 folded, as itts_decode_gemm16x with u/c) AND the attention of itts_attn_decode[_rows]
- * in ONE launch: producer blocks store q/k/v (f32 [R][ldqkv], write-through) and count per head into
- * counters[H] (zeroed by the caller before the launch); attention blocks request their cached K/V
- * first, then wait for their head.  Results equal itts_decode_gemm16x + itts_attn_decode bit for bit.
- * timeout: one word set (never cleared by the library) if a wait gave up.
- * HF modeling_gpt2.py:246-306 (ln_1, c_attn), :54-72 and :185-225 (attention, cache update). */
-int itts_decode_qkv_attn(const void* xh, int64_t ldxh, const void* w_packed16, const float* u, const float* c,
-                         float eps, float* qkv, int64_t ldqkv, void* cache_k, void* cache_v, int64_t cache_bs,
-                         int64_t cache_hs, int smax, const int32_t* pad, int kv_base, const int32_t* tstate, void* out,
-                         int64_t ldo, int R, int H, const int32_t* kv_rows, int64_t ld_rows, uint32_t* counters,
-                         uint32_t* timeout, void* stream);
-/* c_fc (ln_2 folded, gelu) + mlp.c_proj (split-K, ksplit = 8) + the residual reduce in ONE launch:
- * x += proj_b + sum_s partial_s (split order) and xh = bf16(x), equal bit for bit to
- * itts_decode_gemm16x + itts_decode_gemm(epi 2) + itts_residual_reduce_ln (no LayerNorm).
- * counters: [ksplit] group counters then [D/32] column-tile tickets, zeroed before the launch.
- * HF modeling_gpt2.py:229-243 (MLP) and :246-306 (ln_2, residual). */
-int itts_decode_mlp(const void* xh, int64_t ldxh, const void* fc_w16, const float* fc_u, const float* fc_c, float eps,
-                    void* f, int64_t ldf, const void* proj_w, const float* proj_b, float* part, float* x,
-                    int64_t ldx, int R, int D, int ksplit, uint32_t* counters, uint32_t* timeout, void* stream);
+/* ---- the whole decode step (bf16 product mode) ----------------------------------------------- */
 
 /* Weights of one GPT-2 block in the decode packings (engine.fold_ln_weights / pack_skinny[16]). */
 typedef struct ItTsGptLayerW {
@@ -288,11 +268,6 @@ typedef struct ItTsGptDecodeState {
   uint8_t* done;           /* [rows] */
   int32_t* codes;          /* [rows][max_new] */
   const int32_t* forced;   /* teacher forcing (tests) or NULL */
-  void* workspace;         /* itts_gpt_decode_workspace_bytes(); last 16 B: timeout word (zero it once) */
-  int launch_mode;         /* 0: one kernel per phase; 1: the two multi-role launches per layer
-                              (itts_decode_qkv_attn, itts_decode_mlp); 2: as 0, plus each layer's
-                              K/V read ahead on a side stream (forked after the previous layer's
-                              attention, joined before this one's) into the Infinity Cache */
 } ItTsGptDecodeState;
 
 /* Token selection of the step: mode 0 greedy (itts_sample_embed), 1 top-k / top-p sampling
@@ -305,16 +280,18 @@ typedef struct ItTsSampling {
   float top_p;
 } ItTsSampling;
 
-/* Bytes of ItTsGptDecodeState.workspace (hand-off counters + the timeout word), or -1. */
-int64_t itts_gpt_decode_workspace_bytes(const ItTsGptWeights* w);
-/* One whole KV-cached decode step (one HF generate iteration of inference_speech, gpt/model.py:655-708).
- * launch_mode 0, per layer: c_attn with ln_1 folded (itts_decode_gemm16x) -> itts_attn_decode[_rows] ->
- * attn.c_proj (itts_decode_gemm16x residual) -> c_fc with ln_2 folded + gelu -> mlp.c_proj split-K 8
- * (itts_decode_gemm) -> itts_residual_reduce_ln (the last layer's with ln_f + final_norm, Q5).
- * launch_mode 1, per layer: itts_decode_qkv_attn -> attn.c_proj -> itts_decode_mlp (last layer as in
- * mode 0), one memset node zeroing the hand-off counters first.  Then mel_head, token selection + next
- * embedding (modes 0/1 of ItTsSampling) and the step advance.  Graph-capturable: the step counter
- * lives on the device. */
+/* Sizes in bytes of the state buffers for `rows` sequences, in field order: x, xh, qkv, o, f, part,
+ * logits, k_cache, v_cache, pad, tstate, seen, done, codes (ITTS_GPT_STATE_NBUF entries; kv_rows,
+ * forced: caller's choice).  A host without Python allocates these and fills ItTsGptDecodeState. */
+#define ITTS_GPT_STATE_NBUF 14
+int itts_gpt_decode_state_bytes(const ItTsGptWeights* w, int rows, int max_kv, int max_new, int64_t* bytes);
+/* One whole KV-cached decode step (one HF generate iteration of inference_speech, gpt/model.py:655-708),
+ * per layer: c_attn with ln_1 folded (itts_decode_gemm16x) -> itts_attn_decode[_rows] -> attn.c_proj
+ * (itts_decode_gemm16x residual) -> c_fc with ln_2 folded + gelu -> mlp.c_proj split-K 8
+ * (itts_decode_gemm) -> itts_residual_reduce_ln (the last layer's with ln_f + final_norm, Q5); then
+ * mel_head, token selection + next embedding (ItTsSampling modes 0/1) and the step advance.  The
+ * caller's prefill (itts_attn_prefill + the GEMMs above) fills the cache and the first token; rows
+ * padded to whole 32-row tiles in xh / o / f.  Graph-capturable: the step counter lives on the device. */
 int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecodeState* state, const ItTsSampling* sampling,
                          void* stream);
 

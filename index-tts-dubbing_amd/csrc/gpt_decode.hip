@@ -585,7 +585,7 @@ extern "C" int itts_decode_gemm16(const void* a, int64_t lda, const void* w_pack
 //   else:             y = a @ W^T + c
 //   epi 0: store act(y) as out_dtype (act = gelu_tanh if gelu)
 //   epi 1: residual, y is the f32 stream x [M][ldy]: x += y in place, xh[M][ldxh] = bf16(x)
-// nwaves: 4, 8 or 16 waves per workgroup (4: the c_attn of the fused itts_decode_qkv_attn).  A holds whole 32-row tiles (rows >= M are read, never stored);
+// nwaves: 8 or 16 waves per workgroup.  A holds whole 32-row tiles (rows >= M are read, never stored);
 // up to 128 rows share one weight stream.
 extern "C" int itts_decode_gemm16x(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M,
                                    const float* c, const float* u, float eps, int gelu, int epi, void* y, int64_t ldy,
@@ -598,7 +598,7 @@ extern "C" int itts_decode_gemm16x(const void* a, int64_t lda, const void* w_pac
   ITTS_REQUIRE(epi == 0 || epi == 1, fn, "epi must be 0 or 1");
   ITTS_REQUIRE(epi == 0 || (xh && out_dtype == ITTS_F32 && !gelu && !u), fn,
                "residual epilogue: f32 stream, bf16 copy, no activation, no fold");
-  ITTS_REQUIRE(nwaves == 4 || nwaves == 8 || nwaves == 16, fn, "nwaves must be 4, 8 or 16");
+  ITTS_REQUIRE(nwaves == 8 || nwaves == 16, fn, "nwaves must be 8 or 16");
   ITTS_REQUIRE(out_dtype == ITTS_F32 || out_dtype == ITTS_BF16, fn, "unsupported dtype");
   Dg16xArgs d{static_cast<const uint16_t*>(a), lda, static_cast<const u32x4_t*>(w_packed16), K, N, M, c, u, eps, gelu,
               y, ldy, static_cast<uint16_t*>(xh), ldxh};
@@ -612,7 +612,6 @@ extern "C" int itts_decode_gemm16x(const void* a, int64_t lda, const void* w_pac
     else launch_dg16x<NWV, false, 0, float>(d, s);                                          \
   } while (0)
   if (nwaves == 16) DGX(16);
-  else if (nwaves == 4) DGX(4);
   else DGX(8);
 #undef DGX
   return itts::check_launch(fn);

@@ -71,14 +71,12 @@ SIGNATURES = {
     "itts_step_advance": (_c_i, [_vp, _c_i, _vp]),
     "itts_decode_gemm": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _vp,
                                 _c_i64, _c_i, _c_i64, _c_i, _vp]),
-    "itts_decode_qkv_attn": (_c_i, [_vp, _c_i64, _vp, _vp, _vp, _c_f, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_i, _vp,
-                                    _c_i, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _c_i64, _vp, _vp, _vp]),
-    "itts_decode_mlp": (_c_i, [_vp, _c_i64, _vp, _vp, _vp, _c_f, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_i, _c_i,
-                               _c_i, _vp, _vp, _vp]),
-    "itts_gpt_decode_workspace_bytes": (_c_i64, [_vp]),
+    "itts_gpt_decode_state_bytes": (_c_i, [_vp, _c_i, _c_i, _c_i, _vp]),
     "itts_gpt_decode_step": (_c_i, [_vp, _vp, _vp, _vp]),
 }
 
+
+GPT_STATE_NBUF = 14  # itts_gpt_decode_state_bytes() entries
 
 # ---- structs of the whole-step entry point (include/itts_hip.h; field order is the ABI) ----------
 class GptLayerW(ctypes.Structure):
@@ -97,8 +95,7 @@ class GptDecodeState(ctypes.Structure):
     _fields_ = [("rows", _c_i), ("max_kv", _c_i), ("kv_base", _c_i), ("max_new", _c_i)] + \
         [(n, _vp) for n in ("x", "xh", "qkv", "o", "f", "part", "logits", "k_cache", "v_cache", "pad", "tstate",
                             "kv_rows")] + \
-        [("ld_rows", _c_i64)] + [(n, _vp) for n in ("seen", "done", "codes", "forced", "workspace")] + \
-        [("launch_mode", _c_i)]
+        [("ld_rows", _c_i64)] + [(n, _vp) for n in ("seen", "done", "codes", "forced")]
 
 
 class Sampling(ctypes.Structure):

@@ -117,15 +117,11 @@ class HipGPT:
         #  * mlp.c_proj: split-K 8 + reduce launch (default) or one full-K launch of 64 workgroups with
         #    the residual epilogue (ITTS_PROJ_FULLK=1)
         self.proj_fullk = self.fold and os.environ.get("ITTS_PROJ_FULLK", "0") == "1"
-        #  * the whole step as ONE C-ABI call, itts_gpt_decode_step (gpt_step.hip), replaying the same
-        #    launches as _decode_step_fold (ITTS_CSTEP=0: the Python launch sequence); ITTS_MULTIROLE=1:
-        #    its multi-role launches (c_attn + attention, c_fc + mlp.c_proj + reduce in one launch each,
-        #    in-launch hand-offs) -- bit-identical, measured SLOWER (profiles/ubench_fused_r02.txt)
+        #  * the whole step as ONE C-ABI call, itts_gpt_decode_step (gpt_step.hip), launching the same
+        #    kernels as _decode_step_fold (ITTS_CSTEP=0: the Python launch sequence, kept as the test
+        #    reference); multi-role launches and a side-stream K/V prefetch were measured slower
+        #    (profiles/ubench_fused_r02.txt)
         self.cstep = self.fold and os.environ.get("ITTS_CSTEP", "1") != "0"
-        self.multirole = self.cstep and os.environ.get("ITTS_MULTIROLE", "0") == "1"
-        self.qkv_nwaves = 8  # c_attn waves per workgroup (the multi-role launch's producers run 4)
-        #  * ITTS_KV_PREFETCH=1: each layer's K/V read ahead into the Infinity Cache on a side stream
-        self.kv_prefetch = self.cstep and os.environ.get("ITTS_KV_PREFETCH", "0") == "1"
         self.layers: List[_Layer] = []
         for i in range(self.L):
             p = f"gpt.h.{i}"
@@ -352,30 +348,18 @@ class HipGPT:
 
     def _c_state(self, st):
         """ItTsGptDecodeState over one decode state's tensors (rebuilt per call: `forced` may change)."""
-        if "sync" not in st:
-            nb = int(self.lib.itts_gpt_decode_workspace_bytes(ctypes.byref(self._cweights)))
-            st["sync"] = torch.zeros((nb + 3) // 4, dtype=torch.int32, device=self.dev)
         kv_rows = st.get("kv_rows")
         p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         return _hip.GptDecodeState(
             st["B"], self.max_kv, st["s"] + 1, st["max_new"], p(st["x"]), p(st["h"]), p(st["qkv"]), p(st["o"]),
             p(st["f"]), p(st["ws"]), p(st["logits"]), p(st["kc"]), p(st["vc"]), p(st["pad"]), p(st["t"]), p(kv_rows),
             0 if kv_rows is None else kv_rows.stride(0), p(st["seen"]), p(st["done"]), p(st["codes"]),
-            p(st.get("forced")), p(st["sync"]), 1 if self.multirole else (2 if self.kv_prefetch else 0))
-
-    def decode_timed_out(self, st) -> bool:
-        """True if a hand-off wait of the multi-role launches gave up (the step's results are invalid)."""
-        return "sync" in st and bool(st["sync"][-4:].any())
-
-    def _check_timeout(self, st):
-        if self.decode_timed_out(st):
-            st["sync"].zero_()
-            raise _hip.HipError("itts_gpt_decode_step: a hand-off wait timed out (results invalid)")
+            p(st.get("forced")))
 
     def _decode_step_c(self, st, min_new, penalty):
         """bf16 product decode step as ONE C-ABI call (itts_gpt_decode_step, gpt_step.hip): the launches
-        of _decode_step_fold (or the multi-role launches), mel_head, token selection, step advance.
-        Bit-identical to _decode_step_fold (tests/test_gpu_fused.py)."""
+        of _decode_step_fold, mel_head, token selection, step advance.  Bit-identical to
+        _decode_step_fold (tests/test_gpu_cstep.py)."""
         beams = "kv_rows" in st
         smp = st.get("sampling")
         if beams:
@@ -402,7 +386,7 @@ class HipGPT:
         x, h, o, f = st["x"], st["h"], st["o"], st["f"]
         qkv = st["qkv"][: B * 3 * D].view(B, 3 * D)
         for li, ly in enumerate(self.layers):
-            self._dgx(h, ly.wx["qkv"], B, qkv, nwaves=self.qkv_nwaves)
+            self._dgx(h, ly.wx["qkv"], B, qkv)
             kc, vc = st["kc"][li], st["vc"][li]
             rows = st.get("kv_rows")
             if rows is not None:
@@ -437,7 +421,7 @@ class HipGPT:
 
     def _decode_step(self, st, min_new, penalty):
         """One fed token per row -> next token sampled (all device-side; graph-capturable)."""
-        if self.cstep and (st["B"] <= 128 or not self.multirole):
+        if self.cstep:
             return self._decode_step_c(st, min_new, penalty)
         if self.fold:
             return self._decode_step_fold(st, min_new, penalty)
@@ -606,8 +590,7 @@ class HipGPT:
         sampling = (float(temperature), int(top_k), float(top_p)) if do_sample else None
         if do_sample and seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None, self.cstep, self.multirole,
-                self.qkv_nwaves, self.kv_prefetch)
+        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None, self.cstep)
         main = torch.cuda.current_stream(self.dev)
         work = []
         for i, (r0, r1) in enumerate(self._lane_bounds(B, lanes)):
@@ -651,7 +634,6 @@ class HipGPT:
                     break
         for ln in work:
             main.wait_stream(ln["stream"])
-            self._check_timeout(ln["st"])
         codes = torch.cat([ln["st"]["codes"][:, :steps] for ln in work], 0).long()
         hit = codes == self.stop_mel
         if bool(hit.any(dim=1).all()):
@@ -837,8 +819,7 @@ class HipGPT:
         else:
             self._dgw(st["h"], self.head_w, R, self.head_b, st["logits"])
         self._beam_step(st, 0)
-        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep, self.multirole,
-                self.qkv_nwaves, self.kv_prefetch)
+        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep)
         graph_ok = use_graph and max_new_tokens > 1
         if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
             ln["graph"] = (self._capture(st, min_new_tokens, repetition_penalty), gkey)
@@ -862,7 +843,6 @@ class HipGPT:
             steps += 1
             if steps % check_every == 0 and bool(st["done_u"].all()):
                 break
-        self._check_timeout(st)
         return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
 
     def _beam_finalize(self, st, B, K, steps, max_new, length_penalty):

@@ -1,4 +1,4 @@
-"""Per-layer timing of the fused decode launches (gpt_step.hip) against the per-kernel path they
+"""(Historical: needs commit a0a8361, whose multi-role launches were removed afterwards.)  Per-layer
 replace, at the C3 shape (B = 32 rows, KV length ~283, IndexTTS-1.5 weights, all 20 layers' distinct
 weights / caches so the bytes come from HBM as in the real step).  Graph-captured chains of 20
 layers, HIP events, us per layer.  ITTS_HIP_LIB selects a timing build (ITTS_STEP_DIAG) of the

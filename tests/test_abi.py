@@ -76,3 +76,20 @@ def test_product_path_fails_loudly_without_library(tmp_path, monkeypatch):
     with pytest.raises(_hip.HipError, match="no CPU fallback"):
         _hip.load(str(tmp_path / "missing.so"))
     importlib.reload(_hip)
+
+
+def test_step_struct_layouts_match(lib):
+    """ctypes mirrors of ItTsGptLayerW / ItTsGptWeights / ItTsGptDecodeState / ItTsSampling have the
+    C sizes (field order is the ABI), and the state-size query answers without a GPU."""
+    from indextts import _hip
+    for i, c in enumerate((_hip.GptLayerW, _hip.GptWeights, _hip.GptDecodeState, _hip.Sampling)):
+        assert lib.itts_struct_size(i) == ctypes.sizeof(c), c.__name__
+    assert lib.itts_struct_size(99) == -1
+    w = _hip.GptWeights(2, 256, 4, 8194, 8208, 8192, 8193)
+    sizes = (ctypes.c_int64 * _hip.GPT_STATE_NBUF)()
+    assert lib.itts_gpt_decode_state_bytes(ctypes.byref(w), 5, 64, 16, sizes) == 0
+    D, R, Rp = 256, 5, 32
+    assert list(sizes)[:7] == [R * D * 4, Rp * D * 2, R * 3 * D * 4, Rp * D * 2, Rp * 4 * D * 2, 8 * R * D * 4,
+                               R * 8208 * 4]
+    assert sizes[7] == sizes[8] == 2 * R * 4 * 64 * 64 * 2
+    assert lib.itts_gpt_decode_state_bytes(ctypes.byref(w), 0, 64, 16, sizes) != 0

@@ -1,0 +1,128 @@
+"""The decode step driven through the C ABI alone (no HipGPT): a host that only has the header's
+structs and entry points -- as a cgo / JNI / plain-C caller would -- packs the weights, allocates the
+state from ``itts_gpt_decode_state_bytes`` and calls ``itts_gpt_decode_step`` once per token.
+
+Check: teacher-forced decoding of a mel-token sequence from an empty cache (kv_base = 0; the first
+input is mel_emb[start] + mel_pos[0] as after the prefill, token j >= 1 enters as mel_emb[t_j] +
+mel_pos[j + 2], quirk Q1) against an fp32 torch GPT-2 forward of the same sequence (HF
+modeling_gpt2.py:246-306, ln_f + final_norm + mel_head, gpt/model.py:48,180).  bf16 weights and
+activations: per-step logits relative RMS error <= 2e-2; the sampler's recorded argmax equals the
+reference argmax wherever the reference top-1 / top-2 margin exceeds 0.1.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(v):
+    return v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+
+
+def _reference_logits(sd, cfg, tokens, pos):
+    """fp32 GPT-2 over inputs mel_emb[tokens] + mel_pos[pos] ([R, T]); logits [R, T, V]."""
+    D, H = int(cfg.model_dim), int(cfg.heads)
+    x = _t(sd["mel_embedding.weight"]).float()[tokens] + _t(sd["mel_pos_embedding.emb.weight"]).float()[pos]
+    R, T, _ = x.shape
+    mask = torch.full((T, T), float("-inf")).triu(1)
+    for i in range(int(cfg.layers)):
+        p = f"gpt.h.{i}."
+        g = lambda k: _t(sd[p + k]).float()  # noqa: E731
+        h = F.layer_norm(x, (D,), g("ln_1.weight"), g("ln_1.bias"), 1e-5)
+        qkv = h @ g("attn.c_attn.weight") + g("attn.c_attn.bias")
+        q, k, v = (t.view(R, T, H, 64).transpose(1, 2) for t in qkv.split(D, -1))
+        a = torch.softmax(q @ k.transpose(-1, -2) / 8.0 + mask, -1) @ v
+        x = x + a.transpose(1, 2).reshape(R, T, D) @ g("attn.c_proj.weight") + g("attn.c_proj.bias")
+        h = F.layer_norm(x, (D,), g("ln_2.weight"), g("ln_2.bias"), 1e-5)
+        f = F.gelu(h @ g("mlp.c_fc.weight") + g("mlp.c_fc.bias"), approximate="tanh")
+        x = x + f @ g("mlp.c_proj.weight") + g("mlp.c_proj.bias")
+    x = F.layer_norm(x, (D,), _t(sd["gpt.ln_f.weight"]).float(), _t(sd["gpt.ln_f.bias"]).float(), 1e-5)
+    x = F.layer_norm(x, (D,), _t(sd["final_norm.weight"]).float(), _t(sd["final_norm.bias"]).float(), 1e-5)
+    return x @ _t(sd["mel_head.weight"]).float().t() + _t(sd["mel_head.bias"]).float()
+
+
+def test_decode_step_through_the_abi_only():
+    from indextts import _hip
+    from indextts.gpt.engine import fold_ln_weights, pack_skinny
+    from indextts.utils.config import tiny_config
+    from indextts.utils.synthetic import gpt_state_dict
+
+    lib = _hip.load()
+    cfg = tiny_config().gpt
+    sd = gpt_state_dict(cfg, 0, 0.08)
+    dev = "cuda"
+    D, H, L, V = int(cfg.model_dim), int(cfg.heads), int(cfg.layers), int(cfg.number_mel_codes)
+    Vp = (V + 15) // 16 * 16
+    start, stop = int(cfg.start_mel_token), int(cfg.stop_mel_token)
+    keep = []  # device tensors the structs point at
+
+    def dev32(v):
+        t = _t(v).float().contiguous().to(dev)
+        keep.append(t)
+        return t.data_ptr()
+
+    def ln(i, n):
+        return sd[f"gpt.h.{i}.ln_{n}.weight"], sd[f"gpt.h.{i}.ln_{n}.bias"]
+
+    layers = (_hip.GptLayerW * L)()
+    for i in range(L):
+        p = f"gpt.h.{i}."
+        qkv = fold_ln_weights(sd[p + "attn.c_attn.weight"], sd[p + "attn.c_attn.bias"], ln(i, 1), dev)
+        o = fold_ln_weights(sd[p + "attn.c_proj.weight"], sd[p + "attn.c_proj.bias"], None, dev)
+        fc = fold_ln_weights(sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"], ln(i, 2), dev)
+        proj = pack_skinny(_t(sd[p + "mlp.c_proj.weight"]).float().t().contiguous()).to(dev)
+        keep.extend([qkv, o, fc, proj])
+        layers[i] = _hip.GptLayerW(qkv["w16"].data_ptr(), qkv["u"].data_ptr(), qkv["c"].data_ptr(),
+                                   o["w16"].data_ptr(), o["c"].data_ptr(), fc["w16"].data_ptr(), fc["u"].data_ptr(),
+                                   fc["c"].data_ptr(), proj.data_ptr(), dev32(sd[p + "mlp.c_proj.bias"]))
+    head = pack_skinny(_t(sd["mel_head.weight"]).float().contiguous()).to(dev)
+    keep.append(head)
+    w = _hip.GptWeights(L, D, H, V, Vp, start, stop, layers, dev32(sd["gpt.ln_f.weight"]),
+                        dev32(sd["gpt.ln_f.bias"]), dev32(sd["final_norm.weight"]), dev32(sd["final_norm.bias"]),
+                        head.data_ptr(), dev32(sd["mel_head.bias"]), dev32(sd["mel_embedding.weight"]),
+                        dev32(sd["mel_pos_embedding.emb.weight"]))
+
+    R, T, max_kv = 5, 24, 32
+    sizes = (ctypes.c_int64 * _hip.GPT_STATE_NBUF)()
+    assert lib.itts_gpt_decode_state_bytes(ctypes.byref(w), R, max_kv, T, sizes) == 0
+    buf = [torch.zeros(int(n), dtype=torch.uint8, device=dev) for n in sizes]
+    x, xh, qkv, o, f, part, logits, kc, vc, pad, tst, seen, done, codes = buf
+    g = torch.Generator().manual_seed(3)
+    tokens = torch.randint(0, 8192, (R, T), generator=g)
+    tokens[:, 0] = start
+    pos = torch.cat([torch.zeros(R, 1, dtype=torch.long), torch.arange(3, T + 2).expand(R, T - 1)], 1)
+    forced = torch.full((R, T), stop, dtype=torch.int32)
+    forced[:, 1:] = tokens[:, 1:].int()
+    forced = forced.to(dev)
+    # the first input (what the prefill leaves behind): x = mel_emb[start] + mel_pos[0], xh = bf16(x)
+    x0 = (_t(sd["mel_embedding.weight"]).float()[start] + _t(sd["mel_pos_embedding.emb.weight"]).float()[0])
+    x.view(torch.float32).view(R, D).copy_(x0.expand(R, D))
+    xh.view(torch.bfloat16).view(-1, D)[:R].copy_(x0.expand(R, D).to(torch.bfloat16))
+    st = _hip.GptDecodeState(R, max_kv, 0, T, x.data_ptr(), xh.data_ptr(), qkv.data_ptr(), o.data_ptr(),
+                             f.data_ptr(), part.data_ptr(), logits.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                             pad.data_ptr(), tst.data_ptr(), None, 0, seen.data_ptr(), done.data_ptr(),
+                             codes.data_ptr(), forced.data_ptr())
+    smp = _hip.Sampling(0, T, 1.0, 1.0, 0, 1.0)  # greedy, no stop before T, penalty 1 (none)
+    got = []
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(T - 1):
+        _hip.check(lib.itts_gpt_decode_step(ctypes.byref(w), ctypes.byref(st), ctypes.byref(smp), stream),
+                   "itts_gpt_decode_step")
+        got.append(logits.view(torch.float32).view(R, Vp)[:, :V].clone())
+    torch.cuda.synchronize()
+    assert int(tst.view(torch.int32)[0]) == T - 1  # the device step counter advanced once per call
+    got = torch.stack(got, 1).cpu()                                  # [R, T-1, V]
+    ref = _reference_logits(sd, cfg, tokens[:, : T - 1], pos[:, : T - 1])
+    rel = float(((got - ref).pow(2).mean() / ref.pow(2).mean()).sqrt())
+    assert rel <= 2e-2, rel
+    sel = ref.clone()
+    sel[..., stop] = float("-inf")  # min_new_tokens = T suppresses the stop token
+    top2 = sel.topk(2, -1).values
+    margin = top2[..., 0] - top2[..., 1]
+    chosen = codes.view(torch.int32).view(R, T).cpu()[:, 1:T].long()  # argmax recorded at col j + 1
+    ok = (chosen == sel.argmax(-1)) | (margin <= 0.1)
+    assert bool(ok.all()), (chosen, ref.argmax(-1))
