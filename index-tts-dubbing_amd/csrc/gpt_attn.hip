@@ -39,12 +39,14 @@ __device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]
 constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is the caller's
 
 // One workgroup of NT threads per (head, sequence): NT/8 groups of 8 lanes, group g owns keys
-// g, g + NT/8, ...; lane d8 holds dims 8*d8 .. 8*d8+7.  The first round's cached K and V rows (KB = 8
-// keys per group, kept packed: 256 keys at NT = 256) are requested before anything else -- they do
-// not depend on this step's q/k/v -- so their HBM latency overlaps the c_attn slab summation; later
-// rounds (S > 256) load in turn.  Scores via 8-lane shuffles, an online softmax per group (running
-// max m, sum l, partial output o); the groups merge through LDS.  (Measured alternatives, slower at
-// B=32, S~283: 512-thread workgroups; 16 packed keys per group -- 308 VGPRs, 1 wave/SIMD.)
+// g, g + NT/8, ...; lane d8 holds dims 8*d8 .. 8*d8+7.  Issue order: this step's q/k/v, then the
+// round's cached K rows, then its V rows (KB keys per group kept packed in registers: 320 keys per
+// round at NT = 256, KB = 10), so the scores start as soon as K has landed while V still streams;
+// later rounds are requested while the current one computes.  Scores via 8-lane DPP sums, an online
+// softmax per group (running max m, sum l, partial output o); the groups merge through LDS with all
+// NT threads.  (Measured alternatives, slower at B=32, S~283: 512-thread workgroups; 16 packed keys
+// per group -- 308 VGPRs, 1 wave/SIMD; q/k/v requested after the K/V rows: the first score then
+// waited for every K/V byte, 12.7 us at S = 283.)
 // q/k/v = bias + sum of `nsplit` split-K partial slabs of the c_attn GEMM (stride split_stride).
 // ROWS (beam search): key position p of sequence b lives in cache row kv_rows[b * ld_rows + p] (beams
 // share their common prefix, HF's per-step cache reorder becomes this lineage table); this step's
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
   constexpr int RW = sizeof(TC) * 8 / 16;       // 16-B vectors per lane per row (bf16: 1, f32: 2)
   __shared__ float qs[kHD], kn[kHD], vn[kHD];
   __shared__ float gm[NG], gl[NG];
-  __shared__ float pv[NG][kHD + 1];
+  __shared__ float pv[NG + NT / kHD + 1][kHD + 1];  // group partials, then the quarter sums and L
   __shared__ float ofin[PROJ ? kHD : 1];  // PROJ: the merged head output
   const int h = blockIdx.x, b = blockIdx.y;
   const int D = H * kHD;
@@ -98,45 +100,33 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
     else return (int64_t)p * kHD;
   };
   const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
-  // (1) the first round's cached K/V rows do not depend on this step's q/k/v: issue them first
-  u32x4_t kr[KB][RW], vr[KB][RW];
-#pragma unroll
-  for (int u = 0; u < KB; ++u) {
-    const int j = NG * u + g;
-    if (j < nk - 1) {
-#pragma unroll
-      for (int w = 0; w < RW; ++w) {
-        kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + koff(p0 + j) + 8 * d8)[w];
-        vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + koff(p0 + j) + 8 * d8)[w];
-      }
-    }
-  }
-  // (2) q/k/v of this step = bias + sum of the c_attn split-K slabs; new k/v appended to the cache
-  if (threadIdx.x < 3 * kHD) {
-    const int part = threadIdx.x / kHD, d = threadIdx.x - part * kHD;  // 0: q, 1: k, 2: v
-    const int col = part * D + h * kHD + d;
+  // (1) q/k/v of this step (bias + sum of the c_attn split-K slabs) are requested FIRST: loads complete
+  // in issue order, and everything below waits for them, not for the K/V stream behind them
+  const bool qkv_lane = threadIdx.x < 3 * kHD;
+  const int which = threadIdx.x / kHD, dq = threadIdx.x - which * kHD;  // 0: q, 1: k, 2: v
+  const int col = which * D + h * kHD + dq;
+  float sl[4] = {0.f, 0.f, 0.f, 0.f}, qb = 0.f;
+  if (qkv_lane) {
     const float* src = qkv + (int64_t)b * ldqkv + col;
-    float v = qkv_bias ? qkv_bias[col] : 0.f;
-    // up to 4 slabs loaded together (independent loads in flight), summed in slab order
-    float sl[4];
+    qb = qkv_bias ? qkv_bias[col] : 0.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s) sl[s] = s < nsplit ? src[s * split_stride] : 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      if (s < nsplit) v += sl[s];
-    for (int s = 4; s < nsplit; ++s) v += src[s * split_stride];
-    if (part == 0) {
-      qs[d] = v * 0.125f;  // 1/sqrt(64), exact
-    } else if (part == 1) {
-      kn[d] = v;
-      St<TC>::st(Kc + (int64_t)kidx * kHD + d, v);
-    } else {
-      vn[d] = v;
-      St<TC>::st(Vc + (int64_t)kidx * kHD + d, v);
-    }
   }
-  // (2b) PROJ: this head's 64 rows of W, issued after the slab loads so that the wait for the slabs
-  // above does not include them (loads retire in order)
+  // (2) this round's cached K rows, then its V rows (the scores need only K).  Every lane loads a valid
+  // row (key index clamped into the cache), so the loads are unconditional and retire in order; rows
+  // past the round's keys are never used.
+  u32x4_t kr[KB][RW], vr[KB][RW];
+  auto kv_load = [&](u32x4_t (&dst)[KB][RW], const TC* base, int j0) {
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int j = min(j0 + NG * u + g, max(nk - 2, 0));
+#pragma unroll
+      for (int w = 0; w < RW; ++w) dst[u][w] = reinterpret_cast<const u32x4_t*>(base + koff(p0 + j) + 8 * d8)[w];
+    }
+  };
+  kv_load(kr, Kc, 0);
+  kv_load(vr, Vc, 0);
+  // (2b) PROJ: this head's 64 rows of W (needed last: requested last)
   constexpr int PK = PROJ ? kHD / 2 : 1;
   const int kh = threadIdx.x >> 7, pj = threadIdx.x & 127, n0 = 8 * pj;
   u32x4_t wr[PK];
@@ -147,10 +137,31 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
       for (int k = 0; k < PK; ++k) wr[k] = *reinterpret_cast<const u32x4_t*>(wsrc + (int64_t)k * N);
     }
   }
-  __syncthreads();
-  float q[8];
+  // (3) finish q/k/v; this step's k/v appended to the cache
+  if (qkv_lane) {
+    float v = qb;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) q[e] = qs[8 * d8 + e];
+    for (int s = 0; s < 4; ++s)
+      if (s < nsplit) v += sl[s];
+    for (int s = 4; s < nsplit; ++s) v += qkv[(int64_t)b * ldqkv + col + s * split_stride];
+    if (which == 0) {
+      qs[dq] = v * 0.125f;  // 1/sqrt(64), exact
+    } else if (which == 1) {
+      kn[dq] = v;
+      St<TC>::st(Kc + (int64_t)kidx * kHD + dq, v);
+    } else {
+      vn[dq] = v;
+      St<TC>::st(Vc + (int64_t)kidx * kHD + dq, v);
+    }
+  }
+  __syncthreads();
+  float q[8], kme[8], vme[8];  // q, and this step's own key / value (the last key, from LDS)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    q[e] = qs[8 * d8 + e];
+    kme[e] = kn[8 * d8 + e];
+    vme[e] = vn[8 * d8 + e];
+  }
   auto unpack = [&](const u32x4_t (&r)[RW], float (&x)[8]) {
     if constexpr (sizeof(TC) == 2) {
 #pragma unroll
@@ -163,65 +174,58 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
       for (int i = 0; i < 8; ++i) x[i] = __uint_as_float(r[i / 4][i % 4]);
     }
   };
-  // (3) online softmax per 8-lane group over rounds of NG*KB keys (2 rounds at S = 283)
+  // (4) online softmax per 8-lane group over rounds of NG*KB keys.  Software-pipelined: the next
+  // round's K rows are requested as soon as this round's scores no longer need kr, its V rows once
+  // this round's P.V is done.
   float m = -INFINITY, l = 0.f;
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nk; j0 += NG * KB) {
-    if (j0 > 0) {  // later rounds (S > 512): load now
-#pragma unroll
-      for (int u = 0; u < KB; ++u) {
-        const int j = j0 + NG * u + g;
-        if (j < nk - 1) {
-#pragma unroll
-          for (int w = 0; w < RW; ++w) {
-            kr[u][w] = reinterpret_cast<const u32x4_t*>(Kc + koff(p0 + j) + 8 * d8)[w];
-            vr[u][w] = reinterpret_cast<const u32x4_t*>(Vc + koff(p0 + j) + 8 * d8)[w];
-          }
-        }
-      }
-    }
+    const bool more = j0 + NG * KB < nk;
     float s[KB];
     float bm = -INFINITY;
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
       const int j = j0 + NG * u + g;
       float kx[8];
-      if (j < nk - 1) {
-        unpack(kr[u], kx);
-      } else {
+      unpack(kr[u], kx);
+      if (j >= nk - 1) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) kx[e] = kn[8 * d8 + e];  // this step's key (or padding)
+        for (int e = 0; e < 8; ++e) kx[e] = kme[e];  // this step's key (or padding)
       }
-      float part = 0.f;
+      float pt = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) part = fmaf(q[e], kx[e], part);
-      part = sum8_dpp(part);
-      s[u] = j < nk ? part : -INFINITY;
+      for (int e = 0; e < 8; ++e) pt = fmaf(q[e], kx[e], pt);
+      pt = sum8_dpp(pt);
+      s[u] = j < nk ? pt : -INFINITY;
       bm = fmaxf(bm, s[u]);
     }
-    if (bm == -INFINITY) continue;  // this group has no valid key in the round
-    const float mn = fmaxf(m, bm);
-    const float corr = __expf(m - mn);  // m = -inf -> 0
-    l *= corr;
+    if (more) kv_load(kr, Kc, j0 + NG * KB);
+    if (bm != -INFINITY) {  // else this group has no valid key in the round
+      const float mn = fmaxf(m, bm);
+      const float corr = __expf(m - mn);  // m = -inf -> 0
+      l *= corr;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] *= corr;
+      for (int e = 0; e < 8; ++e) o[e] *= corr;
 #pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      const int j = j0 + NG * u + g;
-      const float pr = __expf(s[u] - mn);
-      l += pr;
-      float vx[8];
-      if (j < nk - 1) {
+      for (int u = 0; u < KB; ++u) {
+        const int j = j0 + NG * u + g;
+        const float pr = __expf(s[u] - mn);
+        l += pr;
+        float vx[8];
         unpack(vr[u], vx);
-      } else {
+        if (j >= nk - 1) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) vx[e] = vn[8 * d8 + e];
+          for (int e = 0; e < 8; ++e) vx[e] = vme[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = fmaf(pr, vx[e], o[e]);
       }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = fmaf(pr, vx[e], o[e]);
+      m = mn;
     }
-    m = mn;
+    if (more) kv_load(vr, Vc, j0 + NG * KB);
   }
+  // (5) merge the NG groups: every thread takes the max M, then quarter qd of the block sums groups
+  // 8qd .. 8qd+7 for its dim, the quarters combine in order (fixed-order sums: batch-invariant)
 #pragma unroll
   for (int e = 0; e < 8; ++e) pv[g][8 * d8 + e] = o[e];
   if (d8 == 0) {
@@ -229,16 +233,31 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
     gl[g] = l;
   }
   __syncthreads();
-  if (threadIdx.x < kHD) {
+  constexpr int NQ = NT / kHD, GPQ = NG / NQ;  // quarters, groups per quarter
+  float* qsum = &pv[0][0] + NG * (kHD + 1);     // [NQ][kHD + 1] after pv
+  float* lsum = qsum + NQ * (kHD + 1);          // [NQ]
+  {
+    const int dd = threadIdx.x & (kHD - 1), qd = threadIdx.x / kHD;
     float M = -INFINITY;
 #pragma unroll 8
     for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
     float L = 0.f, acc = 0.f;
-#pragma unroll 8
-    for (int i = 0; i < NG; ++i) {
+#pragma unroll
+    for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
       const float w = __expf(gm[i] - M);  // empty group: exp(-inf) = 0
       L = fmaf(gl[i], w, L);
-      acc = fmaf(pv[i][threadIdx.x], w, acc);
+      acc = fmaf(pv[i][dd], w, acc);
+    }
+    qsum[qd * (kHD + 1) + dd] = acc;
+    if (dd == 0) lsum[qd] = L;
+  }
+  __syncthreads();
+  if (threadIdx.x < kHD) {
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      L += lsum[i];
+      acc += qsum[i * (kHD + 1) + threadIdx.x];
     }
     if constexpr (PROJ) ofin[threadIdx.x] = acc / L;
     else St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, acc / L);

@@ -48,6 +48,33 @@ def _load_state_dict(path: str, key: Optional[str] = None) -> Dict[str, torch.Te
     return sd
 
 
+def _caller_cue_texts(text: str, max_depth: int = 8) -> Optional[List[str]]:
+    """The texts of the cues from ``text`` on, when ``infer`` runs inside a loop over a cue list:
+    srt_dubbing's strategies iterate ``for i, entry in enumerate(entries)`` and call
+    ``tts_engine.synthesize(text=entry.text, ...)`` (srt_dubbing/src/strategies/basic_strategy.py:64-72,
+    stretch / hq_stretch / adaptive likewise) -> ``IndexTTSEngine.synthesize`` -> ``infer``
+    (tts_engines/index_tts_engine.py:45-58).  Found by looking for a local ``entries`` list of objects
+    with a ``text`` attribute in the calling frames; None when there is no such loop."""
+    f = sys._getframe(2)
+    try:
+        for _ in range(max_depth):
+            if f is None:
+                return None
+            ents = f.f_locals.get("entries")
+            if isinstance(ents, (list, tuple)) and ents and all(hasattr(e, "text") for e in ents[:8]):
+                texts = [str(e.text) for e in ents]
+                i = f.f_locals.get("i")
+                if isinstance(i, int) and 0 <= i < len(texts) and texts[i] == text:
+                    return texts[i:]
+                if text in texts:
+                    return texts[texts.index(text):]
+                return None
+            f = f.f_back
+        return None
+    finally:
+        del f
+
+
 class IndexTTS:
     MAX_BATCH = 32
 
@@ -298,9 +325,79 @@ class IndexTTS:
 
     def infer(self, audio_prompt, text, output_path, verbose=False, max_text_tokens_per_sentence=120,
               **generation_kwargs):
-        """infer.py:500-660 -> output_path (16-bit PCM 24 kHz wav written) or (24000, int16 [T, 1])."""
+        """infer.py:500-660 -> output_path (16-bit PCM 24 kHz wav written) or (24000, int16 [T, 1]).
+
+        Cross-call batching for callers that loop over cues one ``infer`` at a time (srt_dubbing's
+        strategies -> ``IndexTTSEngine.synthesize``, unchanged): a result prefetched by ``prefetch``
+        (or by the lookahead below) for the same prompt, text and arguments is returned instead of a
+        new synthesis."""
+        hit = self._take_ahead(audio_prompt, text, max_text_tokens_per_sentence, generation_kwargs)
+        if hit is None and self.LOOKAHEAD > 0:
+            upcoming = _caller_cue_texts(text)
+            if upcoming and len(upcoming) > 1:
+                self.prefetch(audio_prompt, upcoming[: self.LOOKAHEAD], max_text_tokens_per_sentence,
+                              **generation_kwargs)
+                hit = self._take_ahead(audio_prompt, text, max_text_tokens_per_sentence, generation_kwargs)
+        if hit is not None:
+            return self._deliver(hit, output_path)
         return self._synthesize(audio_prompt, text, output_path, verbose, max_text_tokens_per_sentence,
                                 generation_kwargs, fast=False)
+
+    # ------------------------------------------------------------------ cross-call batching
+    # Cues synthesised ahead when ``infer`` is called from inside a loop over a cue list (0: off).
+    LOOKAHEAD = int(os.environ.get("ITTS_LOOKAHEAD", "64"))
+
+    def _ahead_key(self, audio_prompt, max_tokens, gen):
+        try:
+            mtime = os.path.getmtime(audio_prompt) if isinstance(audio_prompt, str) else None
+        except OSError:
+            mtime = None
+        prompt = audio_prompt if isinstance(audio_prompt, str) else id(audio_prompt)
+        return (prompt, mtime, int(max_tokens), tuple(sorted((k, repr(v)) for k, v in gen.items())))
+
+    def _take_ahead(self, audio_prompt, text, max_tokens, gen):
+        ahead = self.__dict__.setdefault("_ahead", {})
+        q = ahead.get((self._ahead_key(audio_prompt, max_tokens, gen), text))
+        if not q:
+            return None
+        res = q.pop(0)  # one result per call: a repeated call synthesises anew (new draws when sampling)
+        if not q:
+            del ahead[(self._ahead_key(audio_prompt, max_tokens, gen), text)]
+        return res
+
+    def prefetch(self, audio_prompt, texts, max_text_tokens_per_sentence=120, **generation_kwargs):
+        """Synthesise ``texts`` now, all sentences of all texts batched (``infer_many``), and keep one
+        result per occurrence for the ``infer`` calls that follow with the same prompt, text and
+        arguments.  Deterministic decoding (``do_sample=False``): each result equals what that
+        ``infer`` call would have computed (rows never interact; tests/test_gpu_lookahead.py); with
+        sampling it is an independent draw from the same distribution, as a fresh call would be."""
+        ahead = self.__dict__.setdefault("_ahead", {})
+        base = self._ahead_key(audio_prompt, max_text_tokens_per_sentence, generation_kwargs)
+        need, have = [], {}
+        for t in texts:
+            have[t] = have.get(t, len(ahead.get((base, t), [])))
+            if have[t] > 0:
+                have[t] -= 1
+            else:
+                need.append(t)
+        if not need:
+            return
+        for t, r in zip(need, self.infer_many(audio_prompt, need, None, False, max_text_tokens_per_sentence,
+                                              **generation_kwargs)):
+            ahead.setdefault((base, t), []).append(r)
+
+    @staticmethod
+    def _deliver(res, output_path):
+        sr, data = res
+        if not output_path:
+            return (sr, data)
+        if os.path.isfile(output_path):
+            os.remove(output_path)
+        if os.path.dirname(output_path) != "":
+            os.makedirs(os.path.dirname(output_path), exist_ok=True)
+        save_wav_int16(output_path, data, sr)
+        print(">> wav file saved to:", output_path)
+        return output_path
 
 
     def infer_many(self, audio_prompt, texts, output_paths=None, verbose=False, max_text_tokens_per_sentence=120,

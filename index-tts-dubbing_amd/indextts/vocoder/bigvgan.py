@@ -164,6 +164,7 @@ class HipBigVGAN:
         self.post_k = wp.shape[-1]
         self.hop = int(np.prod([int(u) for u in h.upsample_rates]))
         self._bufs = {}
+        self._cond_w = {}  # cond_layer / conds[i] weights [out][in] f32 (cond_biases)
         self.fused_amp = True  # narrow stages: activation fused into the conv (False: separate kernels)
 
     # ---------------- per-prompt (cached by the caller) ----------------
@@ -175,11 +176,23 @@ class HipBigVGAN:
 
     @torch.no_grad()
     def cond_biases(self, spk: torch.Tensor):
-        s = spk.float()
-        pre = F.linear(s, self.sd_torch["cond_layer.weight"][:, :, 0], self.sd_torch["cond_layer.bias"])
-        per = [F.linear(s, self.sd_torch[f"conds.{i}.weight"][:, :, 0], self.sd_torch[f"conds.{i}.bias"])
-               for i in range(len(self.ups))]
-        return pre.contiguous(), [p.contiguous() for p in per]
+        """speaker-embedding biases of conv_pre and of each up-sampling stage (the 1x1 convs
+        cond_layer / conds[i] of models.py:184,193-197,224-234) on the exact-f32 GEMM: one fmaf chain
+        per output in k order, so an utterance's biases -- and its waveform -- do not depend on which
+        other utterances share the batch (a BLAS GEMM picks its algorithm by batch size)."""
+        s = spk.float().contiguous()
+        B, K = s.shape
+
+        def lin(name):
+            w = self._cond_w.get(name)
+            if w is None:
+                w = self._cond_w[name] = self.sd_torch[name + ".weight"][:, :, 0].float().contiguous()
+            y = torch.empty(B, w.shape[0], dtype=torch.float32, device=s.device)
+            _hip.check(self.lib.itts_gemm_f32(s.data_ptr(), K, w.data_ptr(), K, B, w.shape[0], K,
+                                              self.sd_torch[name + ".bias"].float().data_ptr(), 0, None,
+                                              y.data_ptr(), w.shape[0], _hip.stream_ptr()), "itts_gemm_f32")
+            return y
+        return lin("cond_layer"), [lin(f"conds.{i}") for i in range(len(self.ups))]
 
     # ---------------- launches ----------------
     def _buf(self, name, shape, dtype=torch.bfloat16):

@@ -1,4 +1,5 @@
-"""(Historical: needs commit a0a8361, whose multi-role launches were removed afterwards.)  Per-layer
+"""(Historical: needs commit a0a8361; its multi-role launches were removed afterwards.)  Per-layer timing of the
+fused decode launches (gpt_step.hip at that commit) against the per-kernel path they
 replace, at the C3 shape (B = 32 rows, KV length ~283, IndexTTS-1.5 weights, all 20 layers' distinct
 weights / caches so the bytes come from HBM as in the real step).  Graph-captured chains of 20
 layers, HIP events, us per layer.  ITTS_HIP_LIB selects a timing build (ITTS_STEP_DIAG) of the

@@ -93,6 +93,38 @@ def test_activation_kernel_bf16_paths_bit_equal_f32_path(C):
         assert bool((yb[b, L:].float() == sentinel).all()) and bool((yf[b, L:] == sentinel).all()), b
 
 
+@pytest.mark.parametrize("i", range(5))
+def test_activation_kernel_f16_bct(golden, i):
+    """f16 in / f16 out through the reference op's argument list (the extension dispatches Half too,
+    type_shim.h:20-43): within 1 f16 ulp of the f32 path on the same (f16-rounded) inputs rounded to
+    f16 -- the arithmetic is f32 in both; the f16 store may fuse the last multiply-add into one
+    rounding (v_fma_mix) where the f32 path rounds twice -- and within f16 rounding of the golden."""
+    _hip, lib = _lib()
+    x = torch.from_numpy(golden[f"act{i}_x"]).half().cuda()
+    f = torch.from_numpy(golden[f"act{i}_filter"]).reshape(-1).cuda()
+    a = torch.from_numpy(golden[f"act{i}_alpha"]).cuda()
+    b = torch.from_numpy(golden[f"act{i}_beta"]).cuda()
+    B, C, T = x.shape
+    yh = torch.empty_like(x)
+    xf = x.float()
+    yf = torch.empty_like(xf)
+    for xin, yout, dt in ((x, yh, _hip.F16), (xf, yf, _hip.F32)):
+        _hip.check(lib.itts_aa_snakebeta_bct(xin.data_ptr(), yout.data_ptr(), f.data_ptr(), f.data_ptr(),
+                                             a.data_ptr(), b.data_ptr(), B, C, T, dt, _hip.stream_ptr()), "bct")
+    torch.cuda.synchronize()
+    hb, fb = yh.cpu().view(torch.int16).int(), yf.cpu().half().view(torch.int16).int()
+    assert int((hb - fb).abs().max()) <= 1 and bool(((hb < 0) == (fb < 0)).all())
+    assert float((hb != fb).float().mean()) < 0.05
+    ref = torch.from_numpy(golden[f"act{i}_y"])
+    tol = 2e-3 * (ref.abs() + torch.from_numpy(golden[f"act{i}_x"]).abs().amax()) + 1e-3
+    assert bool(((yh.cpu().float() - ref).abs() <= tol).all())
+    # f16 in with a non-f16 out (or the reverse) is an argument error, nothing launched
+    rc = lib.itts_aa_snakebeta_fwd(x.data_ptr(), yf.data_ptr(), f.data_ptr(), f.data_ptr(), a.data_ptr(),
+                                   b.data_ptr(), None, B, C, T, C * T, 1, T, C * T, 1, T, _hip.F16, _hip.F32,
+                                   _hip.stream_ptr())
+    assert rc != 0 and b"f16" in lib.itts_last_error()
+
+
 @pytest.mark.parametrize("cin,cout,k,d", [(768, 768, 3, 5), (96, 96, 11, 3), (24, 24, 7, 1), (1024, 1536, 7, 1),
                                           (12, 6, 3, 1), (40, 200, 5, 2)])
 def test_igemm_conv_matches_torch(cin, cout, k, d):
