@@ -180,9 +180,11 @@ int itts_sample_embed(const float* logits, int64_t ldl, int V, uint8_t* seen, ui
                       int64_t ldc, const int32_t* tstate, int col_delta, int min_new, int stop, float penalty,
                       const float* emb, const float* pos_emb, int pos_delta, int D, const float* ln_g,
                       const float* ln_b, float* x, void* h, int h_dtype, int B, const int32_t* forced, void* stream);
-/* do_sample=True variant: Temperature -> TopK (1..64, ties at the k-th value kept) -> TopP warpers
- * and a multinomial draw (HF 4.36 `sample`; infer.py:535-543 defaults top_k 30 / top_p 0.8).
- * top_k == 0 (with top_p == 1): draw from the full softmax.  RNG: counter hash of
+/* do_sample=True variant: Temperature -> TopK (any k >= 1, ties at the k-th value kept; 0 = off) ->
+ * TopP (any top_p, also without TopK) warpers and a multinomial draw (HF 4.36 `sample`; infer.py:535-543
+ * defaults top_k 30 / top_p 0.8).  k <= 64: candidate extraction by repeated block argmax; otherwise
+ * exact thresholds (radix select for TopK, bitwise search of the cumulative mass for TopP) and a
+ * Gumbel-max draw among the survivors.  top_k == 0 and top_p == 1: draw from the full softmax.  RNG: counter hash of
  * (seed = tstate[2] | tstate[3] << 32, row + tstate[1], column) -- statistical parity with
  * torch.multinomial; tstate[1] = global index of this launch's row 0 (row chunks on several streams). */
 int itts_sample_topk_embed(const float* logits, int64_t ldl, int V, uint8_t* seen, uint8_t* done, int32_t* codes,

@@ -21,6 +21,7 @@
 //      _reorder_cache copy of every layer's K/V becomes a copy of 4 B per generated position) --
 //      and writes the next input embedding + ln_1 of each row.
 #include "common.h"
+#include "select.h"
 
 namespace {
 constexpr int kT = 256;
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
   __shared__ float tk_v[kMaxK];
   __shared__ int tk_i[kMaxK];
   __shared__ int ntk;
+  __shared__ int hist[256], bc[2];  // general warper thresholds (select.h)
   const int r = blockIdx.x;
   const int C = 2 * p.K;
   const int col = p.tstate[0] + p.col_delta;
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
   const uint64_t grow = (uint64_t)(uint32_t)(r + p.tstate[1]);
   const uint64_t rkey = mix64(seed ^ mix64((grow << 32) | (uint32_t)col));
 
-  if (!p.do_sample || p.top_k <= 0) {
+  if (!p.do_sample || (p.top_k <= 0 && !(p.top_p < 1.f))) {
     // keys in registers: search -> score; sample without top-k/top-p -> score / T + Gumbel
     if (p.do_sample) {
 #pragma unroll
@@ -219,6 +221,40 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
     if (t < p.V) sc[t] = v[i] * p.inv_temp;
   }
   __syncthreads();
+  if (p.top_k > kMaxK || p.top_k <= 0) {
+    // any top_k, or top-p only: survivors = keys >= the warper threshold (select.h); Gumbel keys of
+    // the survivors in place, then the row's C best keys by C rounds of block argmax
+    const uint32_t T = itts_select::warper_threshold(sc, p.V, p.top_k, p.top_p, 2, hist, bc, rv);
+    for (int t = threadIdx.x; t < p.V; t += kT) {
+      const float x = sc[t];
+      sc[t] = (x == -INFINITY || itts_select::okey(x) < T) ? -INFINITY : x + bs + gumbel(rkey + (uint64_t)t + 1);
+    }
+    __syncthreads();
+    for (int c = 0; c < C; ++c) {
+      float best = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int t = threadIdx.x; t < p.V; t += kT)
+        if (better(sc[t], t, best, bi)) {
+          best = sc[t];
+          bi = t;
+        }
+      block_argmax<kT>(best, bi, rv, ri);
+      if (threadIdx.x == 0) {
+        if (best == -INFINITY) {
+          ck[c] = -INFINITY;
+          cs[c] = -INFINITY;
+          ct[c] = p.stop;
+        } else {
+          ck[c] = best;
+          cs[c] = best - gumbel(rkey + (uint64_t)bi + 1);  // the unperturbed score (incl. the beam's)
+          ct[c] = bi;
+        }
+      }
+      if (best != -INFINITY && (bi % kT) == (int)threadIdx.x) sc[bi] = -INFINITY;
+      __syncthreads();
+    }
+    return;
+  }
   const int kk = p.top_k < 2 ? 2 : p.top_k;
   float mine = -INFINITY;
   int mine_i = 0x7fffffff;
@@ -609,11 +645,10 @@ extern "C" int itts_beam_candidates(const float* logits, int64_t ldl, int V, con
   ITTS_REQUIRE(ldl % 4 == 0 && ldl >= V && ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(seen)) & 15) == 0,
                fn, "logits / seen rows must be 16-B aligned with ldl % 4 == 0");
   ITTS_REQUIRE(!do_sample || temperature > 0.f, fn, "temperature must be > 0");
-  ITTS_REQUIRE(!do_sample || (top_k >= 0 && top_k <= kMaxK), fn, "top_k must be in [0, 64]");
-  ITTS_REQUIRE(!do_sample || top_k > 0 || top_p >= 1.f, fn, "top_p < 1 needs 0 < top_k <= 64");
+  ITTS_REQUIRE(!do_sample || top_k >= 0, fn, "top_k must be >= 0");
   BeamArgs a{logits, ldl, V, const_cast<uint8_t*>(seen), beam_score, tstate, col_delta, min_new, stop, penalty,
              do_sample, do_sample ? 1.f / temperature : 1.f, top_k, top_p, num_beams, cand_key, cand_score, cand_tok};
-  const size_t lds = (do_sample && top_k > 0) ? (size_t)V * sizeof(float) : 0;
+  const size_t lds = (do_sample && (top_k > 0 || top_p < 1.f)) ? (size_t)V * sizeof(float) : 0;
   ITTS_REQUIRE(lds <= 64 * 1024 - 2048, fn, "vocabulary too large for the LDS score buffer");
   hipLaunchKernelGGL(beam_cand_kernel, dim3(R), dim3(kT), lds, itts::as_stream(stream), a);
   return itts::check_launch(fn);

@@ -15,6 +15,7 @@
 // The column index comes from a device counter (tstate[0] + col_delta) so a captured hipGraph
 // replays the identical launch every step; itts_step_advance bumps the counter.
 #include "common.h"
+#include "select.h"
 
 namespace {
 constexpr int kT = 256;
@@ -215,10 +216,11 @@ __global__ __launch_bounds__(kT) void sample_embed_kernel(SampleArgs p) {
                        p.pos_delta, p.D, p.g, p.bta, p.x, reinterpret_cast<TH*>(p.h), &tok_s, rv);
 }
 
-// do_sample: scores (after processors, / temperature) staged in LDS; the top-k candidates are
-// extracted in descending order by repeated block argmax (each thread caches the max of its own
-// strided slice, only the winner rescans); top-p + the multinomial draw run on the <= kMaxK
-// candidates.  top_k == 0: no top-k / top-p, Gumbel-max draw over the whole vocabulary.
+// do_sample: scores (after processors, / temperature) staged in LDS.  0 < top_k <= 64: the top-k
+// candidates are extracted in descending order by repeated block argmax (each thread caches the max
+// of its own strided slice, only the winner rescans); top-p + the multinomial draw run on the
+// candidates.  top_k > 64 or top-p alone: warper thresholds (select.h) + a Gumbel-max draw among the
+// survivors.  top_k == 0 and top_p == 1: Gumbel-max draw over the whole vocabulary.
 template <typename TH>
 __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
   extern __shared__ float sc[];  // [V]
@@ -226,6 +228,7 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
   __shared__ int ri[kT / 64];
   __shared__ float cv[kMaxK];
   __shared__ int ci[kMaxK];
+  __shared__ int hist[256], bc[2];  // general warper thresholds (select.h)
   __shared__ int tok_s;
   const int b = blockIdx.x;
   const int col = p.tstate[0] + p.col_delta;
@@ -236,7 +239,23 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
   uint8_t* sr = p.seen + (int64_t)b * p.ldl;
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  if (p.top_k <= 0) {  // plain multinomial == argmax(score + Gumbel noise)
+  if (p.top_k > kMaxK || (p.top_k <= 0 && p.top_p < 1.f)) {
+    // any top_k, or top-p only: warper thresholds over the staged row (select.h), then a Gumbel-max
+    // draw among the survivors == a multinomial draw from their renormalised softmax
+    for (int v = threadIdx.x; v < p.V; v += kT) sc[v] = processed_score(p, lr, sr, v, col) * p.inv_temp;
+    __syncthreads();
+    const uint32_t T = itts_select::warper_threshold(sc, p.V, p.top_k, p.top_p, 1, hist, bc, rv);
+    for (int v = threadIdx.x; v < p.V; v += kT) {
+      const float s = sc[v];
+      if (s == -INFINITY || itts_select::okey(s) < T) continue;
+      const float gmb = s - __logf(-__logf(uniform01(key + (uint64_t)v + 1)));
+      if (better(gmb, v, best, bi)) {
+        best = gmb;
+        bi = v;
+      }
+    }
+    block_argmax(best, bi, rv, ri);
+  } else if (p.top_k <= 0) {  // plain multinomial == argmax(score + Gumbel noise)
     for (int v = threadIdx.x; v < p.V; v += kT) {
       const float s = processed_score(p, lr, sr, v, col) * p.inv_temp;
       const float gmb = s - __logf(-__logf(uniform01(key + (uint64_t)v + 1)));
@@ -349,10 +368,9 @@ int launch_sample(const char* fn, SampleArgs& p, int h_dtype, int B, bool do_sam
     else
       hipLaunchKernelGGL((sample_embed_kernel<float, false>), dim3(B), dim3(kT), 0, s, p);
   } else {
-    ITTS_REQUIRE(p.top_k >= 0 && p.top_k <= kMaxK, fn, "top_k must be in [0, 64]");
-    ITTS_REQUIRE(p.top_k > 0 || p.top_p >= 1.f, fn, "top_p < 1 needs 0 < top_k <= 64");
+    ITTS_REQUIRE(p.top_k >= 0, fn, "top_k must be >= 0");
     ITTS_REQUIRE(p.inv_temp > 0.f, fn, "temperature must be > 0");
-    const size_t lds = p.top_k > 0 ? (size_t)p.V * sizeof(float) : 0;
+    const size_t lds = (p.top_k > 0 || p.top_p < 1.f) ? (size_t)p.V * sizeof(float) : 0;
     ITTS_REQUIRE(lds <= 64 * 1024 - 1024, fn, "vocabulary too large for the LDS score buffer");
     if (h_dtype == ITTS_BF16)
       hipLaunchKernelGGL(sample_topk_embed_kernel<uint16_t>, dim3(B), dim3(kT), lds, s, p);

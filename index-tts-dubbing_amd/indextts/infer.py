@@ -229,8 +229,6 @@ class IndexTTS:
             smp = dict(num_beams=num_beams, length_penalty=float(length_penalty or 0.0))
         if do_sample:
             top_k = int(top_k or 0)
-            if top_k > 64 or (top_k == 0 and top_p is not None and top_p < 1.0):
-                raise ValueError("HIP sampler supports 1 <= top_k <= 64 (or top_k=0 with top_p=1)")
             smp.update(do_sample=True, temperature=float(temperature), top_k=top_k,
                        top_p=1.0 if top_p is None else float(top_p), seed=seed)
         return dict(max_mel_tokens=int(max_mel_tokens), repetition_penalty=float(repetition_penalty),

@@ -87,10 +87,12 @@ def test_bf16_beam_search_batch_invariant_and_close(beam_golden):
     np.testing.assert_array_equal(alone[0, :4], bg["full_codes"][0, :4])
 
 
-def test_beam_sample_distribution_matches_oracle(beam_golden):
-    """tiny config, reference defaults (top_k 30, top_p 0.8, T 1, 3 beams), 3 steps: total-variation
-    distance between the GPU's and the oracle's first-token distributions <= 0.12 (600 GPU samples
-    in one batched call vs 400 oracle samples)."""
+@pytest.mark.parametrize("top_k,top_p", [(30, 0.8), (0, 0.8), (100, 1.0)])
+def test_beam_sample_distribution_matches_oracle(beam_golden, top_k, top_p):
+    """tiny config, reference defaults (top_k 30, top_p 0.8, T 1, 3 beams) and the general warper
+    path (top-p only; top_k > 64), 3 steps: total-variation distance between the GPU's and the
+    oracle's first-token distributions <= 0.12 (600 GPU samples in one batched call vs 400 oracle
+    samples)."""
     from oracle.gpt_oracle import GPTOracle
     bg = beam_golden
     eng = _engine("tiny", "f32", 0.0, bg)
@@ -98,10 +100,10 @@ def test_beam_sample_distribution_matches_oracle(beam_golden):
     text = torch.from_numpy(bg["tiny_text"])
     N = 600
     got = eng.generate(conds.cuda(), text.cuda().expand(N, -1).contiguous(), 3, num_beams=3, do_sample=True,
-                       top_k=30, top_p=0.8, seed=123).cpu().numpy()
+                       top_k=top_k, top_p=top_p, seed=123).cpu().numpy()
     orc = GPTOracle(_sd("tiny", 0.0, bg), _cfg("tiny").gpt)
     gen = torch.Generator().manual_seed(0)
-    ref = [int(orc.generate_beam(conds, text, 3, do_sample=True, top_k=30, top_p=0.8, generator=gen)[0, 0])
+    ref = [int(orc.generate_beam(conds, text, 3, do_sample=True, top_k=top_k, top_p=top_p, generator=gen)[0, 0])
            for _ in range(400)]
     pg = np.bincount(got[:, 0], minlength=8194) / N
     pr = np.bincount(np.array(ref), minlength=8194) / len(ref)
@@ -109,5 +111,5 @@ def test_beam_sample_distribution_matches_oracle(beam_golden):
     assert tv <= 0.12, (tv, np.argsort(-pg)[:5], np.sort(-pg)[:5], np.argsort(-pr)[:5], np.sort(-pr)[:5])
     # different seeds -> different draws; same seed -> same draws
     again = eng.generate(conds.cuda(), text.cuda().expand(N, -1).contiguous(), 3, num_beams=3, do_sample=True,
-                         top_k=30, top_p=0.8, seed=123).cpu().numpy()
+                         top_k=top_k, top_p=top_p, seed=123).cpu().numpy()
     np.testing.assert_array_equal(again, got)

@@ -178,7 +178,10 @@ def _draw(logits_row, B, calls, temperature, top_k, top_p, seed0=1):
 
 
 @pytest.mark.parametrize("temperature,top_k,top_p", [(1.0, 30, 0.8), (0.7, 30, 0.8), (1.0, 5, 1.0),
-                                                     (1.3, 64, 0.95), (1.0, 0, 1.0)])
+                                                     (1.3, 64, 0.95), (1.0, 0, 1.0),
+                                                     # general warper thresholds (select.h): any top_k, top-p only
+                                                     (1.0, 100, 0.9), (1.0, 0, 0.7), (0.8, 1000, 1.0),
+                                                     (1.0, 8194, 0.5), (1.0, 65, 1.0)])
 def test_sampling_distribution(temperature, top_k, top_p):
     g = torch.Generator().manual_seed(0)
     V = 8194
@@ -192,6 +195,19 @@ def test_sampling_distribution(temperature, top_k, top_p):
     sig = torch.sqrt(p.double() * (1 - p.double()) / N)
     bad = (f - p.double()).abs() > 5 * sig + 2e-3
     assert not bool(bad.any()), (f[bad][:5], p[bad][:5])
+
+
+def test_sampling_general_path_keeps_ties_and_top_only():
+    """radix-select top_k (> 64) keeps every score tied with the k-th; top_p -> 0 keeps the top token."""
+    V = 1000
+    logits = torch.full((V,), -10.0)
+    logits[:70] = torch.linspace(6.0, 5.0, 70)
+    logits[[700, 701]] = float(logits[68])  # tied with the 69th largest (k = 69 -> 71 survivors)
+    counts = _draw(logits, 256, 16, 1.0, 69, 1.0)
+    assert int(counts[:69].sum() + counts[[700, 701]].sum()) == int(counts.sum())
+    assert int(counts[69:700].sum()) == 0
+    counts = _draw(logits, 256, 2, 1.0, 0, 1e-6)
+    assert int(counts[0]) == int(counts.sum())
 
 
 def test_sampling_keeps_ties_at_kth_value():
