@@ -34,7 +34,8 @@ const char* itts_last_error(void);
 int itts_abi_version(void);
 const char* itts_build_target(void); /* "gfx950" */
 /* sizeof of the ABI structs below (0 ItTsGptLayerW, 1 ItTsGptWeights, 2 ItTsGptDecodeState,
- * 3 ItTsSampling), -1 otherwise: lets a binding check its struct layouts. */
+ * 3 ItTsSampling, 4 ItTsConv, 5 ItTsAct, 6 ItTsAmpLayer, 7 ItTsBigvganStage, 8 ItTsBigvganWeights),
+ * -1 otherwise: lets a binding check its struct layouts. */
 int64_t itts_struct_size(int which);
 
 /* ---- BigVGAN2 vocoder ----------------------------------------------------------------------- */
@@ -85,6 +86,53 @@ int itts_amp_conv_fwd(const void* x, int64_t x_sb, int64_t ldx, const float* up1
 int itts_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* w, float bias, int C, int K,
                         const int32_t* lengths, int B, int Tmax, float* wav, int16_t* pcm, int64_t y_sb,
                         int dtype_in, void* stream);
+
+/* The whole generator (BigVGAN.forward, models.py:201-250, + the int16 conversion of infer.py:627-631)
+ * as one call.  Weights in the packings above: every conv as an igemm-packed tap list. */
+typedef struct ItTsConv {
+  const void* w;          /* [ntaps][co_pad][ci_pad] bf16 (itts_igemm_pack_dims) */
+  const float* bias;      /* [cout] */
+  int cin, cout, ntaps;
+  int32_t tap_off[16];    /* y[t] = sum_j W_j x[t + tap_off[j]] */
+} ItTsConv;
+typedef struct ItTsAct {  /* Activation1d(SnakeBeta): 12-tap filters, log-scale alpha / beta [C] */
+  const float *up12, *down12, *log_alpha, *log_beta;
+} ItTsAct;
+typedef struct ItTsAmpLayer {  /* one AMPBlock1 dilation: x' = c2(a2(c1(a1(x)))) + x */
+  ItTsAct a1;
+  ItTsConv c1;
+  ItTsAct a2;
+  ItTsConv c2;
+} ItTsAmpLayer;
+typedef struct ItTsBigvganStage {
+  int up_rate;                 /* ConvTranspose1d stride u: u polyphase convs */
+  const ItTsConv* phases;      /* [up_rate] */
+  const float* cond_w;         /* conds[i] (1x1 on the speaker embedding): [cout][spk_dim] f32 */
+  const float* cond_b;         /* [cout] */
+  int n_blocks, n_layers;      /* resblocks (kernel sizes) x dilations */
+  const ItTsAmpLayer* layers;  /* [n_blocks][n_layers] */
+  int amp_mode;                /* 0: act kernel + implicit-GEMM conv; 1: act fused into itts_amp_conv_fwd;
+                                  2: act kernel + itts_amp_conv_fwd without activation */
+} ItTsBigvganStage;
+typedef struct ItTsBigvganWeights {
+  int n_stages, gpt_dim, spk_dim;
+  ItTsConv conv_pre;
+  const float* cond_pre_w;     /* cond_layer: [conv_pre.cout][spk_dim] f32 */
+  const float* cond_pre_b;
+  const ItTsBigvganStage* stages;  /* HOST array [n_stages] */
+  ItTsAct act_post;
+  const float* post_w;         /* conv_post [C][post_k] f32 */
+  float post_b;
+  int post_k;
+} ItTsBigvganWeights;
+/* Workspace bytes of itts_bigvgan_forward for B utterances of at most T latent frames, or -1. */
+int64_t itts_bigvgan_workspace_bytes(const ItTsBigvganWeights* w, int B, int T);
+/* latent [B][T][gpt_dim] bf16 (rows >= lengths[b] ignored), lengths [B] frames (device), spk [B][spk_dim]
+ * f32 -> wav [B][T*hop] f32 (tanh output) and, if pcm != NULL, pcm [B][T*hop] int16 (Q8); samples past
+ * lengths[b]*hop undefined.  Per utterance exactly as at batch 1 (ragged-exact edges; speaker biases on
+ * the exact-f32 GEMM).  Replaces BigVGAN.forward (models.py:201-250) with weight norm folded. */
+int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* latent, const int32_t* lengths, const float* spk,
+                         int B, int T, void* workspace, float* wav, int16_t* pcm, void* stream);
 
 /* ---- prompt front-end ------------------------------------------------------------------------- */
 

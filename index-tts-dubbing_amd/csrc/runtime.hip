@@ -31,13 +31,18 @@ extern "C" int itts_abi_version(void) { return 1; }
 extern "C" const char* itts_build_target(void) { return "gfx950"; }
 
 // sizeof of the ABI structs (include/itts_hip.h), so bindings can check their layouts:
-// 0 ItTsGptLayerW, 1 ItTsGptWeights, 2 ItTsGptDecodeState, 3 ItTsSampling
+// 0 ItTsGptLayerW, 1 ItTsGptWeights, 2 ItTsGptDecodeState, 3 ItTsSampling, 4-8 the vocoder structs
 extern "C" int64_t itts_struct_size(int which) {
   switch (which) {
     case 0: return sizeof(ItTsGptLayerW);
     case 1: return sizeof(ItTsGptWeights);
     case 2: return sizeof(ItTsGptDecodeState);
     case 3: return sizeof(ItTsSampling);
+    case 4: return sizeof(ItTsConv);
+    case 5: return sizeof(ItTsAct);
+    case 6: return sizeof(ItTsAmpLayer);
+    case 7: return sizeof(ItTsBigvganStage);
+    case 8: return sizeof(ItTsBigvganWeights);
     default: return -1;
   }
 }

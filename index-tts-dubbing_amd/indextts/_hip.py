@@ -73,6 +73,8 @@ SIGNATURES = {
                                 _c_i64, _c_i, _c_i64, _c_i, _vp]),
     "itts_gpt_decode_state_bytes": (_c_i, [_vp, _c_i, _c_i, _c_i, _vp]),
     "itts_gpt_decode_step": (_c_i, [_vp, _vp, _vp, _vp]),
+    "itts_bigvgan_workspace_bytes": (_c_i64, [_vp, _c_i, _c_i]),
+    "itts_bigvgan_forward": (_c_i, [_vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _vp, _vp]),
 }
 
 
@@ -163,3 +165,28 @@ def dtype_code(t) -> int:
 def i32_array(vals):
     arr = (ctypes.c_int32 * len(vals))(*[int(v) for v in vals])
     return arr
+
+
+# ---- structs of the whole-vocoder entry point (include/itts_hip.h) --------------------------------
+class Conv(ctypes.Structure):
+    _fields_ = [("w", _vp), ("bias", _vp), ("cin", _c_i), ("cout", _c_i), ("ntaps", _c_i),
+                ("tap_off", ctypes.c_int32 * 16)]
+
+
+class Act(ctypes.Structure):
+    _fields_ = [("up12", _vp), ("down12", _vp), ("log_alpha", _vp), ("log_beta", _vp)]
+
+
+class AmpLayer(ctypes.Structure):
+    _fields_ = [("a1", Act), ("c1", Conv), ("a2", Act), ("c2", Conv)]
+
+
+class BigvganStage(ctypes.Structure):
+    _fields_ = [("up_rate", _c_i), ("phases", ctypes.POINTER(Conv)), ("cond_w", _vp), ("cond_b", _vp),
+                ("n_blocks", _c_i), ("n_layers", _c_i), ("layers", ctypes.POINTER(AmpLayer)), ("amp_mode", _c_i)]
+
+
+class BigvganWeights(ctypes.Structure):
+    _fields_ = [("n_stages", _c_i), ("gpt_dim", _c_i), ("spk_dim", _c_i), ("conv_pre", Conv), ("cond_pre_w", _vp),
+                ("cond_pre_b", _vp), ("stages", ctypes.POINTER(BigvganStage)), ("act_post", Act), ("post_w", _vp),
+                ("post_b", _c_f), ("post_k", _c_i)]

@@ -17,6 +17,7 @@ PyTorch ops on the device and cached by the caller (quirk Q6).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from typing import Dict, List
@@ -166,6 +167,55 @@ class HipBigVGAN:
         self._bufs = {}
         self._cond_w = {}  # cond_layer / conds[i] weights [out][in] f32 (cond_biases)
         self.fused_amp = True  # narrow stages: activation fused into the conv (False: separate kernels)
+        # the whole forward as ONE C-ABI call (itts_bigvgan_forward, bigvgan_fwd.hip) launching the same
+        # kernels as _forward_py (ITTS_VOC_CFORWARD=0: the Python launch sequence, the test reference)
+        self.cforward = os.environ.get("ITTS_VOC_CFORWARD", "1") != "0"
+        self._cw = self._c_weights()
+        self._ws = None
+
+    # ---------------- the C-ABI description of this generator ----------------
+    @staticmethod
+    def _c_conv(c: "_Conv") -> "_hip.Conv":
+        offs = (ctypes.c_int32 * 16)(*list(c.offs))
+        return _hip.Conv(c.w.data_ptr(), _hip.ptr(c.bias), c.cin, c.cout, c.ntaps, offs)
+
+    @staticmethod
+    def _c_act(a: "_Act") -> "_hip.Act":
+        return _hip.Act(a.up.data_ptr(), a.down.data_ptr(), a.alpha.data_ptr(), a.beta.data_ptr())
+
+    def _amp_mode(self, C: int) -> int:
+        if self.fused_amp and C in self.FUSED_CHANNELS:
+            return 1
+        if self.fused_amp and C in self.SPLIT_CHANNELS:
+            return 2
+        return 0
+
+    def _c_weights(self):
+        """ItTsBigvganWeights over this generator's packed tensors (arrays kept alive on the struct)."""
+        for name in ["cond_layer"] + [f"conds.{i}" for i in range(len(self.ups))]:
+            if name not in self._cond_w:
+                self._cond_w[name] = self.sd_torch[name + ".weight"][:, :, 0].float().contiguous()
+        keep = []
+        stages = (_hip.BigvganStage * len(self.ups))()
+        for i, (u, phases) in enumerate(self.ups):
+            ph = (_hip.Conv * u)(*[self._c_conv(c) for c in phases])
+            blocks = self.blocks[i]
+            nl = len(blocks[0])
+            lay = (_hip.AmpLayer * (len(blocks) * nl))()
+            for j, layers in enumerate(blocks):
+                for n, (a1, c1, a2, c2) in enumerate(layers):
+                    lay[j * nl + n] = _hip.AmpLayer(self._c_act(a1), self._c_conv(c1), self._c_act(a2), self._c_conv(c2))
+            cb = self.sd_torch[f"conds.{i}.bias"].float()
+            keep += [ph, lay, cb]
+            stages[i] = _hip.BigvganStage(u, ph, self._cond_w[f"conds.{i}"].data_ptr(), cb.data_ptr(), len(blocks), nl,
+                                          lay, self._amp_mode(phases[0].cout))
+        pb = self.sd_torch["cond_layer.bias"].float()
+        keep += [stages, pb]
+        w = _hip.BigvganWeights(len(self.ups), self.conv_pre.cin, self._cond_w["cond_layer"].shape[1],
+                                self._c_conv(self.conv_pre), self._cond_w["cond_layer"].data_ptr(), pb.data_ptr(),
+                                stages, self._c_act(self.act_post), self.post_w.data_ptr(), self.post_b, self.post_k)
+        w._keep = keep
+        return w
 
     # ---------------- per-prompt (cached by the caller) ----------------
     @torch.no_grad()
@@ -235,6 +285,32 @@ class HipBigVGAN:
     def forward(self, latent: torch.Tensor, lengths: torch.Tensor, spk: torch.Tensor, want_pcm: bool = True):
         """latent [B, T, gpt_dim] (bf16/f32, device), lengths [B] frames, spk [B, spk_dim]
         -> (wav f32 [B, T*hop], pcm int16 [B, T*hop] or None); samples past lengths*hop are undefined."""
+        if not self.cforward:
+            return self._forward_py(latent, lengths, spk, want_pcm)
+        x = latent.to(self.device)
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        x = x.contiguous()
+        B, T, _ = x.shape
+        self.rows = int(lengths.sum()) * self.hop  # output rows (host-side, for accounting)
+        lens = lengths.to(self.device, torch.int32).contiguous()
+        s = spk.to(self.device).float().contiguous()
+        nb = int(self.lib.itts_bigvgan_workspace_bytes(ctypes.byref(self._cw), B, T))
+        if nb < 0:
+            raise _hip.HipError("itts_bigvgan_workspace_bytes: bad sizes")
+        if self._ws is None or self._ws.numel() < nb:
+            self._ws = None
+            self._ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        wav = torch.empty(B, T * self.hop, dtype=torch.float32, device=self.device)
+        pcm = torch.empty(B, T * self.hop, dtype=torch.int16, device=self.device) if want_pcm else None
+        _hip.check(self.lib.itts_bigvgan_forward(ctypes.byref(self._cw), x.data_ptr(), lens.data_ptr(), s.data_ptr(),
+                                                 B, T, self._ws.data_ptr(), wav.data_ptr(), _hip.ptr(pcm),
+                                                 _hip.stream_ptr()), "itts_bigvgan_forward")
+        return wav, pcm
+
+    @torch.no_grad()
+    def _forward_py(self, latent: torch.Tensor, lengths: torch.Tensor, spk: torch.Tensor, want_pcm: bool = True):
+        """The same launches from Python (reference for tests/test_gpu_vocoder.py's C-ABI test)."""
         dev = self.device
         x = latent.to(dev)
         if x.dtype != torch.bfloat16:

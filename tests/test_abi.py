@@ -82,7 +82,8 @@ def test_step_struct_layouts_match(lib):
     """ctypes mirrors of ItTsGptLayerW / ItTsGptWeights / ItTsGptDecodeState / ItTsSampling have the
     C sizes (field order is the ABI), and the state-size query answers without a GPU."""
     from indextts import _hip
-    for i, c in enumerate((_hip.GptLayerW, _hip.GptWeights, _hip.GptDecodeState, _hip.Sampling)):
+    for i, c in enumerate((_hip.GptLayerW, _hip.GptWeights, _hip.GptDecodeState, _hip.Sampling, _hip.Conv, _hip.Act,
+                           _hip.AmpLayer, _hip.BigvganStage, _hip.BigvganWeights)):
         assert lib.itts_struct_size(i) == ctypes.sizeof(c), c.__name__
     assert lib.itts_struct_size(99) == -1
     w = _hip.GptWeights(2, 256, 4, 8194, 8208, 8192, 8193)

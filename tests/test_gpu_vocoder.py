@@ -164,6 +164,27 @@ def _vocoder(tag):
 
 
 @pytest.mark.parametrize("tag", ["tiny", "full"])
+def test_vocoder_c_forward_equals_python_launches(tag):
+    """itts_bigvgan_forward (the whole generator as one C-ABI call, bigvgan_fwd.hip) == the Python launch
+    sequence of the same kernels (HipBigVGAN._forward_py), bit for bit: ragged batch (incl. a 1-frame
+    utterance), random latents and speaker embeddings."""
+    voc, _ = _vocoder(tag)
+    g = torch.Generator().manual_seed(11)
+    B, T = 3, 9 if tag == "tiny" else 6
+    lat = (torch.randn(B, T, voc.conv_pre.cin, generator=g) * 0.5).to(torch.bfloat16).cuda()
+    lens = torch.tensor([T, 1, T - 2], dtype=torch.int32)
+    spk = torch.randn(B, voc._cond_w["cond_layer"].shape[1], generator=g).cuda()
+    voc.cforward = True
+    wav_c, pcm_c = voc.forward(lat, lens, spk)
+    wav_p, pcm_p = voc._forward_py(lat, lens, spk)
+    torch.cuda.synchronize()
+    for b in range(B):
+        n = int(lens[b]) * voc.hop
+        assert torch.equal(wav_c[b, :n].cpu(), wav_p[b, :n].cpu()), b
+        assert torch.equal(pcm_c[b, :n].cpu(), pcm_p[b, :n].cpu()), b
+
+
+@pytest.mark.parametrize("tag", ["tiny", "full"])
 def test_vocoder_matches_reference_golden(golden, tag):
     voc, _ = _vocoder(tag)
     lat = torch.from_numpy(golden[f"{tag}_bv_latent"]).cuda()
