@@ -36,8 +36,8 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 # PMC traffic summaries of the CURRENT build (profiles/run_profiles.sh; FETCH_SIZE x2 per
 # MI355X_MICROARCH.md, calibrated by profiles/pmc_calibrate.py); None when not yet measured
-TRAFFIC_DECODE = "traffic_decode_r02.json"
-TRAFFIC_VOCODER = "traffic_vocoder_r02.json"
+TRAFFIC_DECODE = "traffic_decode_r02b.json"
+TRAFFIC_VOCODER = "traffic_vocoder_r02b.json"
 
 
 class KernelTimer:
@@ -82,6 +82,27 @@ def install_conv_timer(voc, timer):
         return timer.wrap(lambda: orig(c, x, y, lens, **kw), 2.0 * rows * c.cout * c.cin * c.ntaps, nbytes)
 
     voc._conv = timed
+
+
+def install_hbm_timers(voc, t_act, t_amp):
+    """HIP events around the standalone activation launches and the fused act+conv launches (C = 24 /
+    48), with their algorithmic HBM bytes: valid rows x channels, each element read once and written
+    once (+ residual rows read; + the packed weights once)."""
+    orig_act, orig_amp = voc._act, voc._amp
+
+    def act(a, x, y, lens):
+        nbytes = 2.0 * voc.rows * x.shape[2] * 2
+        return t_act.wrap(lambda: orig_act(a, x, y, lens), 0.0, nbytes)
+
+    def amp(c, x, y, lens, a=None, r1=None, r2=None, alpha=1.0):
+        if a is None:  # conv-only variant (C = 96): not the HBM-bound fused kernel
+            return orig_amp(c, x, y, lens, a, r1, r2, alpha)
+        nres = (r1 is not None) + (r2 is not None)
+        nbytes = 2.0 * voc.rows * (c.cin + c.cout * (1 + nres)) + 2.0 * c.ntaps * c.cin * c.cout
+        return t_amp.wrap(lambda: orig_amp(c, x, y, lens, a, r1, r2, alpha), 2.0 * voc.rows * c.cout * c.cin * c.ntaps,
+                          nbytes)
+
+    voc._act, voc._amp = act, amp
 
 
 def _traffic(name, key):
@@ -234,8 +255,9 @@ def main():
     if args.workload == "c5":
         return long_form(args, cfg, gsd, vsd, dev, world, rank)
     tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + L + 2 + 1 + N + 8)
-    timer = KernelTimer()
+    timer, t_act, t_amp = KernelTimer(), KernelTimer(), KernelTimer()
     install_conv_timer(tts.vocoder, timer)
+    install_hbm_timers(tts.vocoder, t_act, t_amp)
     # global batch of B * world utterances; utterance i runs on rank i % world (weak scaling)
     mels, texts = make_inputs(cfg, shard(B * world, world, rank), L, args.prompt_frames)
     mels = [m.to(dev) for m in mels]
@@ -280,10 +302,12 @@ def main():
         # the vocoder runs as ONE C-ABI call (itts_bigvgan_forward) in the timed steps; its implicit-GEMM
         # launches are timed one by one in an extra, untimed step through the Python launch sequence
         # (the same kernels, HipBigVGAN._forward_py)
-        tts.vocoder.cforward, timer.enabled = False, True
+        tts.vocoder.cforward = False
+        timer.enabled = t_act.enabled = t_amp.enabled = True
         step()
         torch.cuda.synchronize()
-        tts.vocoder.cforward, timer.enabled = True, False
+        timer.enabled = t_act.enabled = t_amp.enabled = False
+        tts.vocoder.cforward = True
     k_ms, k_flops, k_n = timer.result()
     dec = None
     if step_ev:
@@ -316,6 +340,19 @@ def main():
            "avg_launch_us": round(1e3 * k_ms / max(k_n, 1), 2),
            "algorithmic_bytes_per_launch": round(timer.bytes / max(k_n, 1)),
            "share_of_step": round(k_ms / (1e3 * dt / args.steps), 3)}
+    hbm = {}
+    for key, t, name, tkey in (("roofline_vocoder_act", t_act, "itts_aa_snakebeta_fwd (Activation1d, C >= 96 stages "
+                                "and activation_post)", "aa_snakebeta_bytes_per_launch"),
+                               ("roofline_vocoder_amp", t_amp, "itts_amp_conv_fwd (Activation1d fused into the "
+                                "AMPBlock1 convs, C = 24 / 48)", "amp_conv_bytes_per_launch")):
+        ms, _, n = t.result()
+        if n:
+            gbs = t.bytes / (ms * 1e-3) / 1e9
+            hbm[key] = {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": _traffic(TRAFFIC_VOCODER, tkey),
+                        "launches": n, "avg_launch_us": round(1e3 * ms / n, 2),
+                        "algorithmic_bytes_per_launch": round(t.bytes / n),
+                        "share_of_step": round(ms / (1e3 * dt / args.steps), 3)}
     if dec is not None and args.decoding == "greedy":  # the decode step: the dominant unit of work
         dec["traffic"] = _traffic(TRAFFIC_DECODE, "bytes_per_step")
     cpu = None
@@ -339,6 +376,7 @@ def main():
                    "global_batch": B * world, "seq_len": N, "parallelism": f"dp{world}"},
         "roofline": dec,
         "roofline_vocoder_conv": voc,
+        **hbm,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -12,7 +12,8 @@ rm -rf /tmp/prof /tmp/pmc_*
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof -o run -- \
     python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof_$TAG.log 2>&1
 cp "$(find /tmp/prof -name '*kernel_stats.csv' | head -n 1)" gpurun_out/kernel_stats_$TAG.csv
-python3 profiles/summarize.py gpurun_out/kernel_stats_$TAG.csv 2 > gpurun_out/kernel_stats_$TAG.txt
+# 4 batches under the profiler: warmup 1 + timed 2 + bench.py's instrumented vocoder step 1
+python3 profiles/summarize.py gpurun_out/kernel_stats_$TAG.csv 4 > gpurun_out/kernel_stats_$TAG.txt
 if [ "${2:-pmc}" = "pmc" ]; then
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pmc_df -o run -- python3 profiles/pmc_decode.py > gpurun_out/pmc_df.log 2>&1
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pmc_dw -o run -- python3 profiles/pmc_decode.py > gpurun_out/pmc_dw.log 2>&1
@@ -22,5 +23,13 @@ if [ "${2:-pmc}" = "pmc" ]; then
   python3 profiles/traffic.py vocoder /tmp/pmc_vf /tmp/pmc_vw > gpurun_out/traffic_vocoder_$TAG.json
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pmc_c -o run -- python3 profiles/pmc_calibrate.py > gpurun_out/pmc_c.log 2>&1
   python3 profiles/traffic.py calibrate /tmp/pmc_c > gpurun_out/traffic_calibration_$TAG.json
+  # what bounds the vocoder's HBM-bound kernels: wave-state and instruction counters (two passes)
+  timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+      SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --output-format csv \
+      -d /tmp/pmc_vsq -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vsq.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES --output-format csv \
+      -d /tmp/pmc_vsi -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vsi.log 2>&1
+  { python3 profiles/pmc_summary.py /tmp/pmc_vsq amp_conv aa_snakebeta igemm;
+    python3 profiles/pmc_summary.py /tmp/pmc_vsi amp_conv aa_snakebeta igemm; } > gpurun_out/pmc_sq_vocoder_$TAG.txt
 fi
 echo profiles-done

@@ -19,6 +19,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 DECODE_KERNELS = ("attn_decode_kernel", "decode_gemm_kernel", "decode_gemm16_kernel", "decode_gemm16x_kernel",
@@ -47,8 +48,11 @@ def short(name):
 
 def vocoder(fetch, write):
     out = {"kernel": "igemm_kernel (BigVGAN convs, second of two C3 vocoder forwards)"}
-    for name in ("igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel"):
-        ids = sorted(k for k, (n, _) in fetch.items() if name in n and k in write)
+    groups = {"igemm_kernel": lambda n: "igemm_kernel" in n,
+              "amp_conv_kernel": lambda n: bool(re.search(r"amp_conv_kernel<[^>]*true>", n)),  # act fused
+              "aa_snakebeta_kernel": lambda n: "aa_snakebeta_kernel" in n}
+    for name, match in groups.items():
+        ids = sorted(k for k, (n, _) in fetch.items() if match(n) and k in write)
         ids = ids[len(ids) // 2:]
         if not ids:
             continue
@@ -57,6 +61,8 @@ def vocoder(fetch, write):
         out[name] = {"dispatches": len(ids), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                      "bytes_per_launch": fb + wb}
     out["igemm_bytes_per_launch"] = out.get("igemm_kernel", {}).get("bytes_per_launch")
+    out["amp_conv_bytes_per_launch"] = out.get("amp_conv_kernel", {}).get("bytes_per_launch")
+    out["aa_snakebeta_bytes_per_launch"] = out.get("aa_snakebeta_kernel", {}).get("bytes_per_launch")
     out["correction"] = "FETCH_SIZE x2 (gfx950 coalesced-read undercount); KiB -> bytes"
     return out
 

@@ -147,8 +147,11 @@ def test_decoding_kwargs():
         IndexTTS._decoding(dict(num_beams=9))
     g = IndexTTS._decoding(dict(do_sample=False, num_beams=1, max_mel_tokens=64))
     assert g == dict(max_mel_tokens=64, repetition_penalty=10.0, min_new_tokens=0)
-    with pytest.raises(ValueError):
-        IndexTTS._decoding(dict(do_sample=True, num_beams=1, top_k=0, top_p=0.5))
+    # top-p alone and top_k > 64 are supported (exact warper thresholds, csrc/select.h)
+    s = IndexTTS._decoding(dict(do_sample=True, num_beams=1, top_k=0, top_p=0.5))
+    assert (s["top_k"], s["top_p"], "num_beams" in s) == (0, 0.5, False)
+    s = IndexTTS._decoding(dict(do_sample=True, num_beams=3, top_k=200))
+    assert (s["top_k"], s["num_beams"]) == (200, 3)
 
 
 def test_cli_argument_checks(tmp_path, capsys):
