@@ -13,8 +13,10 @@
 // One workgroup = 256 threads = a [TT x CT] (time x channel) output tile; the raw input window
 // [TT+12 x CT] is staged once through LDS as f32 (replicate-clamped rows), then each thread runs a
 // 16-output register window along time for one channel (HBM-bound: 1 read + 1 write per element).
+#include <cstdlib>
 #include <type_traits>
 
+#include "act_mfma.h"
 #include "common.h"
 
 namespace {
@@ -174,6 +176,99 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
   }
 }
 
+// ---- bf16 channel-last path with both FIRs on MFMA (act_mfma.h) ----
+// Workgroup = 4 waves = NB 32-channel blocks x (4 / NB) strips of S output tiles (32 rows each):
+// TT = (4 / NB) * 32 * S output rows x NB * 32 channels.  The window [TT + 32 rows][NB * 64 B] holds
+// x rows t0 - 7 .. t0 + TT + 24 (rows the FIRs weight by zero are zero-filled, not loaded), replicate-
+// clamped per utterance.  Interior outputs leave straight from the down product's accumulators
+// (8-B stores of 4 channels); outputs within 3 samples of an utterance edge, where the down-sampler's
+// own replicate pad applies, are recomputed by the VALU formula from the same window.
+template <int NB, int S>
+__global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p) {
+  constexpr int PX = NB * 64, NS = 4 / NB, TT = NS * 32 * S, WROWS = TT + 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char win[];
+  const int b = blockIdx.z;
+  const int len = p.lens ? p.lens[b] : p.T;
+  const int t0 = blockIdx.y * TT;
+  if (t0 >= len) return;
+  const int c0 = blockIdx.x * NB * 32;
+  const uint16_t* x = reinterpret_cast<const uint16_t*>(p.x) + (int64_t)b * p.sxb;
+  uint16_t* y = reinterpret_cast<uint16_t*>(p.y) + (int64_t)b * p.syb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // ---- window: rows 1 .. TT + 12 (t0 - 6 .. t0 + TT + 5) loaded, the rest zero ----
+  constexpr int CV = NB * 4;  // 16-B vectors per row
+  constexpr int NV = (WROWS * CV + 255) / 256;
+  u32x4_t buf[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = tid + 256 * i;
+    buf[i] = u32x4_t{0u, 0u, 0u, 0u};
+    const int r = v / CV, c = (v - r * CV) * 8;
+    if (v < WROWS * CV && r >= 1 && r <= TT + 12 && c0 + c < p.C) {
+      const int t = min(max(t0 - 7 + r, 0), len - 1);
+      buf[i] = *reinterpret_cast<const u32x4_t*>(x + (int64_t)t * p.sxt + c0 + c);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = tid + 256 * i;
+    const int r = v / CV, c = (v - r * CV) * 8;
+    if (v < WROWS * CV) *reinterpret_cast<u32x4_t*>(win + itts_actm::woff<PX>(r, c)) = buf[i];
+  }
+  float* tl = reinterpret_cast<float*>(win + WROWS * PX);  // 12 up taps, 12 down taps
+  if (tid < 24) tl[tid] = tid < 12 ? p.up[tid] : p.down[tid - 12];
+  __syncthreads();
+
+  // ---- strips ----
+  const int blk = wave % NB, sidx = wave / NB;
+  const int cb = 32 * blk;                 // window column of the block
+  const int ts = t0 + sidx * 32 * S;       // first output of the strip
+  const int ntile = min(S, max(0, (len - ts + 31) / 32));
+  {
+    itts_actm::Taps T;
+    itts_actm::make_taps(tl, T);
+    const int ch = c0 + cb + (lane & 31);
+    const float a_rev = ch < p.C ? expf(p.log_alpha[ch]) * 0.15915494309189535f : 0.f;
+    const float inv_b = ch < p.C ? 1.0f / (expf(p.log_beta[ch]) + 1e-9f) : 0.f;
+    const int h = lane >> 5;
+    itts_actm::strip<PX>(win, sidx * 32 * S, cb, ntile, T, a_rev, inv_b, [&](int i, const f32x16_t& acc) {
+      const int t = ts + 32 * i + (lane & 31);
+      if (t < 3 || t >= len - 3) return;  // edges: VALU fix-up below
+      uint16_t* yr = y + (int64_t)t * p.syt + c0 + cb + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (c0 + cb + 8 * g + 4 * h < p.C) {
+          const u32x2_t o{pack2bf(acc[4 * g], acc[4 * g + 1]), pack2bf(acc[4 * g + 2], acc[4 * g + 3])};
+          *reinterpret_cast<u32x2_t*>(yr + 8 * g) = o;
+        }
+      }
+    });
+  }
+
+  // ---- outputs within 3 samples of an utterance edge (uniform per block) ----
+  if (t0 < 3 || t0 + TT > len - 3) {
+    const int te = min(t0 + TT, len);
+    for (int it = tid; it < 6 * NB * 32; it += 256) {
+      const int e = it / (NB * 32), cc = it - e * (NB * 32);
+      const int t = e < 3 ? e : len - 6 + e;
+      if (t < t0 || t >= te || t < 0 || (e >= 3 && t < 3) || c0 + cc >= p.C) continue;
+      const float a = expf(p.log_alpha[c0 + cc]) * 0.15915494309189535f;
+      const float inv_b = 1.0f / (expf(p.log_beta[c0 + cc]) + 1e-9f);
+      y[(int64_t)t * p.syt + c0 + cc] = f2bf(itts_actm::exact_at<PX>(win, t0 - 7, t, len, cc, tl, a, inv_b));
+    }
+  }
+}
+
+template <int NB, int S>
+void launch_mfma(const ActArgs& a, hipStream_t s) {
+  constexpr int TT = (4 / NB) * 32 * S;
+  const int nblk = (a.C + 31) / 32;
+  dim3 grid((nblk + NB - 1) / NB, (a.T + TT - 1) / TT, a.B);
+  const size_t lds = (size_t)(TT + 32) * NB * 64 + 24 * sizeof(float);
+  hipLaunchKernelGGL((aa_snake_mfma_kernel<NB, S>), grid, dim3(256), lds, s, a);
+}
+
 template <typename TI, typename TO>
 void launch(const ActArgs& a, bool vec, bool vout, hipStream_t s) {
   dim3 grid((a.T + a.nsub * kTO - 1) / (a.nsub * kTO), (a.C + a.CT - 1) / a.CT, a.B);
@@ -196,6 +291,15 @@ void launch(const ActArgs& a, bool vec, bool vout, hipStream_t s) {
 }
 
 }  // namespace
+
+// ITTS_ACT_MFMA=0 selects the VALU kernel for the bf16 channel-last layout too (A/B measurements)
+bool act_mfma_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ITTS_ACT_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, const float* down12,
                                      const float* log_alpha, const float* log_beta, const int32_t* lengths,
@@ -222,7 +326,13 @@ extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, 
   const bool vout = dtype_out == ITTS_BF16 && y_sc == 1 && C % 8 == 0 && y_st % 8 == 0 && y_sb % 8 == 0 &&
                     (reinterpret_cast<uintptr_t>(y) & 15) == 0;
   if (dtype_in == ITTS_F16) launch<_Float16, _Float16>(a, false, false, s);  // f32 math, RNE half stores
-  else if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, vout, s);
+  else if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16 && vec && vout && act_mfma_enabled()) {
+    // the vocoder's layout: both FIRs on MFMA
+    const int nblk = (C + 31) / 32;
+    if (nblk % 4 == 0) launch_mfma<4, 4>(a, s);
+    else if (nblk % 2 == 0) launch_mfma<2, 4>(a, s);
+    else launch_mfma<1, 4>(a, s);
+  } else if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, vout, s);
   else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, false, false, s);
   else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, false, vout, s);
   else launch<uint16_t, float>(a, vec, false, s);

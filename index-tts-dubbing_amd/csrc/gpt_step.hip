@@ -15,7 +15,8 @@
 // producers' weight loads queue behind the consumers' streams and every in-launch hand-off (sc1
 // stores, drain, counter, poll) cost more than the kernel boundary it replaced; K/V read ahead into
 // the Infinity Cache on a side stream: attention with cache-resident K/V is 9.7 vs 12.7 us, but the
-// side stream slowed the whole step from 830 to 1327 us.
+// side stream slowed the whole step from 830 to 1327 us; each kernel requesting a later kernel's
+// weights into the Infinity Cache in-kernel (profiles/prefetch_ab_r02.txt): every plan slower.
 #include "common.h"
 
 namespace {

@@ -15,6 +15,17 @@ g = torch.Generator().manual_seed(0)
 lat = torch.randn(B, T, 1024, generator=g).to("cuda", torch.bfloat16)
 spk = torch.randn(B, 512, generator=g).cuda()
 lens = torch.full((B,), T, dtype=torch.int32)
+# whole generator as one C call (the product path), then per-launch timings through the Python
+# launch sequence (same kernels)
+for it in range(3):
+    torch.cuda.synchronize()
+    c0 = torch.cuda.Event(enable_timing=True); c1 = torch.cuda.Event(enable_timing=True)
+    c0.record()
+    voc.forward(lat, lens, spk)
+    c1.record()
+    torch.cuda.synchronize()
+print(f"vocoder forward (C call): {c0.elapsed_time(c1):.1f} ms")
+voc.cforward = False
 stats = collections.defaultdict(lambda: [0, 0.0, 0.0])
 events = []
 for name in ("_conv", "_amp", "_act"):

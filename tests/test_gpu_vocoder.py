@@ -62,11 +62,16 @@ def test_activation_kernel_ragged_channel_last():
 
 
 @pytest.mark.parametrize("C", [24, 48, 96, 192, 768])
-def test_activation_kernel_bf16_paths_bit_equal_f32_path(C):
-    """bf16 in / bf16 out (16-B staged loads + LDS-tiled 16-B row stores) == the f32 in / f32 out
-    path on the same values, rounded to bf16 (RNE): the math is identical f32, only the staging
-    and the store differ.  Ragged rows cover a partial last time tile (len - t0 < tile), a row
-    shorter than the filter halo (len < 6) and a one-sample row; rows >= len stay untouched."""
+def test_activation_kernel_bf16_mfma_path_vs_f32_path(C):
+    """bf16 channel-last in / out (the vocoder's layout) runs both FIRs on MFMA (act_mfma.h) with the
+    taps split into bf16 hi + lo and the SnakeBeta output rounded to bf16 before the down-sampler.
+    vs the f32 VALU path on the same values: |d| <= 2^-7 |y| + 5e-3 rms(y) per element (one bf16 ulp
+    of the output plus the 2^-9 rounding of the intermediate, which scales with |SnakeBeta(u)|, not
+    |y|, carried through the 12-tap low-pass) and rms(d) <= 3e-3 rms(y) (the output rounding alone
+    is ~1.1e-3);
+    the 3 outputs at each utterance edge (VALU fix-up) are the f32 path rounded, bit for bit.
+    Ragged rows cover a partial last time tile (len - t0 < tile), a row shorter than the filter
+    halo (len < 6) and a one-sample row; rows >= len stay untouched."""
     from indextts.utils.synthetic import kaiser_sinc_lowpass
     _hip, lib = _lib()
     torch.manual_seed(C)
@@ -87,10 +92,20 @@ def test_activation_kernel_bf16_paths_bit_equal_f32_path(C):
                                              T * C, C, 1, dt, dt, _hip.stream_ptr()), "fwd")
     torch.cuda.synchronize()
     yb, yf = yb.cpu(), yf.cpu()
+    rms = float(yf[0].pow(2).mean().sqrt())
     for b in range(B):
         L = int(lens[b])
-        assert torch.equal(yb[b, :L].view(torch.int16), yf[b, :L].to(torch.bfloat16).view(torch.int16)), b
+        got, ref = yb[b, :L].float(), yf[b, :L]
+        err = (got - ref).abs()
+        bound = 2.0 ** -7 * ref.abs() + 5e-3 * rms
+        assert bool((err <= bound).all()), (b, float((err - bound).max()))
+        assert float(err.pow(2).mean().sqrt()) <= 3e-3 * rms, b
+        edge = sorted({t for t in (0, 1, 2, L - 3, L - 2, L - 1) if 0 <= t < L})
+        assert torch.equal(yb[b, edge].view(torch.int16), yf[b, edge].to(torch.bfloat16).view(torch.int16)), b
         assert bool((yb[b, L:].float() == sentinel).all()) and bool((yf[b, L:] == sentinel).all()), b
+    # most outputs are the f32 path rounded exactly
+    same = (yb[0].view(torch.int16) == yf[0].to(torch.bfloat16).view(torch.int16)).float().mean()
+    assert float(same) > 0.6, float(same)
 
 
 @pytest.mark.parametrize("i", range(5))
