@@ -16,11 +16,18 @@
 // through double-buffered LDS (row pitch padded by 16 B -> conflict-free ds_read_b128 fragments),
 // with a 3-deep register ring (K-step it+2's global loads in flight while step it computes).
 // Tiles are remapped XCD-aware (output-channel tiles of one row tile run together on one XCD).
+// WIN (convs of >= 5 taps, tap span <= 64 rows): K steps run channel chunk outer, tap inner, and the A
+// operand of a chunk is ONE input window of TM + span rows staged once for all its taps (tap j reads
+// it at row offset off_j - min_off), instead of TM rows per tap: an 11-tap conv moves 178 input rows
+// per chunk through L2 -> LDS instead of 1408.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
 
 constexpr int kMaxTaps = 16;
+constexpr int kWinSpan = 64;  // WIN: max tap span (rows)
 
 struct IgArgs {
   const uint16_t* x;
@@ -36,6 +43,7 @@ struct IgArgs {
   int ymul, yoff;
   float alpha;
   int gelu;
+  int min_off, span;  // WIN: smallest tap offset, window rows beyond TM
   int tap_off[kMaxTaps];
 };
 
@@ -44,13 +52,14 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
 }
 
-template <int TM, int TN, int WM, int WN, int KC, bool VEC, typename OutT>
+template <int TM, int TN, int WM, int WN, int KC, bool VEC, typename OutT, bool WIN = false>
 __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArgs p) {
   constexpr int NT = 64 * (TM / WM) * (TN / WN);  // threads (one wave per WM x WN sub-tile)
   constexpr int PITCH = KC * 2 + 16;            // bytes per LDS row
-  constexpr int A_BYTES = TM * PITCH, B_BYTES = TN * PITCH;
+  constexpr int AR = WIN ? TM + kWinSpan : TM;  // A rows staged per buffer
+  constexpr int A_BYTES = AR * PITCH, B_BYTES = TN * PITCH;
   constexpr int VPR = KC / 8;                   // 16-B vectors per row
-  constexpr int A_TOT = TM * VPR, B_TOT = TN * VPR;  // 16-B vectors per tile
+  constexpr int A_TOT = AR * VPR, B_TOT = TN * VPR;  // 16-B vectors per tile (A: upper bound)
   constexpr int A_VEC = (A_TOT + NT - 1) / NT, B_VEC = (B_TOT + NT - 1) / NT;
   constexpr int FM = WM / 32, FN = WN / 32;     // MFMA tiles per wave
   constexpr int WAVES_N = TN / WN;
@@ -76,19 +85,32 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
 
   // 3-deep register ring: the global loads of K-step it+2 are issued while step it computes, so
   // every load has two steps of MFMAs (plus the other block's) to arrive before its LDS write.
+  // WIN: the ring carries B only; a chunk's window goes through one register set (loaded at the
+  // step two before the chunk's first, written at the step before) into ONE LDS window buffer.
   struct Stage {
-    u32x4_t a[A_VEC], b[B_VEC];
+    u32x4_t a[WIN ? 1 : A_VEC], b[B_VEC];
   };
   Stage S0, S1, S2;
-  auto gload = [&](int it, Stage& r) {
-    const int j = it / nchunks, c0 = (it - j * nchunks) * KC;
-    const int toff = p.tap_off[j];
+  u32x4_t wa[WIN ? A_VEC : 1];
+  // K step it -> (tap j, channel chunk c0): tap outer (per-tap A tiles) or, WIN, chunk outer
+  auto kstep = [&](int it, int& j, int& c0) {
+    if (WIN) {
+      const int c = it / p.ntaps;
+      j = it - c * p.ntaps;
+      c0 = c * KC;
+    } else {
+      j = it / nchunks;
+      c0 = (it - j * nchunks) * KC;
+    }
+  };
+  const int a_rows = WIN ? TM + p.span : TM;
+  auto aload = [&](u32x4_t* dst, int toff, int c0) {
 #pragma unroll
     for (int i = 0; i < A_VEC; ++i) {
       const int v = tid + NT * i, row = v / VPR, cv = (v % VPR) * 8;
       const int t = q0 + row + toff, c = c0 + cv;
       u32x4_t val = {0u, 0u, 0u, 0u};
-      if (v < A_TOT && t >= 0 && t < len) {
+      if (row < a_rows && v < A_TOT && t >= 0 && t < len) {
         const uint16_t* src = X + (int64_t)t * p.ldx + c;
         if (VEC) {
           if (c < p.Cin) val = *reinterpret_cast<const u32x4_t*>(src);
@@ -99,7 +121,16 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
           val = u32x4_t{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
         }
       }
-      r.a[i] = val;
+      dst[i] = val;
+    }
+  };
+  auto gload = [&](int it, Stage& r) {
+    int j, c0;
+    kstep(it, j, c0);
+    if (WIN) {
+      if (j == 0) aload(wa, p.min_off, c0);
+    } else {
+      aload(r.a, p.tap_off[j], c0);
     }
     const uint16_t* Wj = p.w + ((int64_t)j * p.co_pad + n0) * p.ci_pad + c0;
 #pragma unroll
@@ -108,13 +139,23 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
       if (v < B_TOT) r.b[i] = *reinterpret_cast<const u32x4_t*>(Wj + (int64_t)row * p.ci_pad + cv);
     }
   };
-  auto swrite = [&](int buf, const Stage& r) {
-    unsigned char* As = smem + buf * (A_BYTES + B_BYTES);
-    unsigned char* Bs = As + A_BYTES;
+  // LDS: per-tap mode [A 0][B 0][A 1][B 1]; WIN [window][B 0][B 1]
+  auto abase = [&](int it) -> unsigned char* {
+    return WIN ? smem : smem + (it & 1) * (A_BYTES + B_BYTES);
+  };
+  auto bbase = [&](int it) -> unsigned char* {
+    return WIN ? smem + A_BYTES + (it & 1) * B_BYTES : smem + (it & 1) * (A_BYTES + B_BYTES) + A_BYTES;
+  };
+  auto swrite = [&](int it, const Stage& r) {
+    unsigned char* As = abase(it);
+    unsigned char* Bs = bbase(it);
+    if (!WIN || it % p.ntaps == 0) {
+      const u32x4_t* src = WIN ? wa : r.a;
 #pragma unroll
-    for (int i = 0; i < A_VEC; ++i) {
-      const int v = tid + NT * i, row = v / VPR, cv = v % VPR;
-      if (v < A_TOT) *reinterpret_cast<u32x4_t*>(As + row * PITCH + cv * 16) = r.a[i];
+      for (int i = 0; i < A_VEC; ++i) {
+        const int v = tid + NT * i, row = v / VPR, cv = v % VPR;
+        if (v < A_TOT && row < a_rows) *reinterpret_cast<u32x4_t*>(As + row * PITCH + cv * 16) = src[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_VEC; ++i) {
@@ -132,15 +173,21 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int r32 = lane & 31, h = lane >> 5;
-  auto compute = [&](int buf) {
-    const unsigned char* As = smem + buf * (A_BYTES + B_BYTES);
-    const unsigned char* Bs = As + A_BYTES;
+  auto compute = [&](int it) {
+    const unsigned char* As = abase(it);
+    const unsigned char* Bs = bbase(it);
+    int arow = 0;  // WIN: this tap's first window row
+    if (WIN) {
+      int j, c0;
+      kstep(it, j, c0);
+      arow = p.tap_off[j] - p.min_off;
+    }
 #pragma unroll
     for (int ks = 0; ks < KC / 16; ++ks) {
       bf16x8_t af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8_t*>(As + (wm + 32 * i + r32) * PITCH + ks * 32 + h * 16);
+        af[i] = *reinterpret_cast<const bf16x8_t*>(As + (arow + wm + 32 * i + r32) * PITCH + ks * 32 + h * 16);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
         bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn + 32 * j + r32) * PITCH + ks * 32 + h * 16);
@@ -154,9 +201,10 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
   // the other buffer (last read in step it-1, fenced by that step's barrier), barrier
   auto step = [&](int it, Stage& ld, const Stage& wr) {
     if (it + 2 < kiters) gload(it + 2, ld);
-    compute(it & 1);
+    compute(it);
     if (it + 1 < kiters) {
-      swrite((it + 1) & 1, wr);
+      if (WIN && (it + 1) % p.ntaps == 0) __syncthreads();  // every wave is done with the window
+      swrite(it + 1, wr);
       __syncthreads();
     }
   };
@@ -199,11 +247,27 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
   }
 }
 
+// ITTS_IGEMM_WIN=0 keeps the per-tap A tiles (A/B measurements)
+bool igemm_win_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ITTS_IGEMM_WIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int TM, int TN, int WM, int WN, int KC, typename OutT>
 void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
   dim3 grid(((a.Tmax + TM - 1) / TM) * ((a.Cout + TN - 1) / TN) * a.B);
-  size_t lds = 2 * (size_t)(TM + TN) * (KC * 2 + 16);
   constexpr int NT = 64 * (TM / WM) * (TN / WN);
+  // the window form for convs of >= 5 taps on the vectorised path (span within the staged rows);
+  // at 3 taps the extra barrier per chunk outweighs the saved loads (profiles/ubench_vocoder_r02_win.txt)
+  if (vec && a.ntaps >= 5 && a.span <= kWinSpan && igemm_win_enabled()) {
+    const size_t lds = (size_t)(TM + kWinSpan + 2 * TN) * (KC * 2 + 16);
+    hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT, true>), grid, dim3(NT), lds, s, a);
+    return;
+  }
+  const size_t lds = 2 * (size_t)(TM + TN) * (KC * 2 + 16);
   if (vec)
     hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT>), grid, dim3(NT), lds, s, a);
   else
@@ -271,7 +335,14 @@ extern "C" int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const vo
   a.yoff = y_row_off;
   a.alpha = alpha;
   a.gelu = gelu;
-  for (int j = 0; j < ntaps; ++j) a.tap_off[j] = tap_off[j];
+  int lo = tap_off[0], hi = tap_off[0];
+  for (int j = 0; j < ntaps; ++j) {
+    a.tap_off[j] = tap_off[j];
+    lo = tap_off[j] < lo ? tap_off[j] : lo;
+    hi = tap_off[j] > hi ? tap_off[j] : hi;
+  }
+  a.min_off = lo;
+  a.span = hi - lo;
   const bool vec = (Cin % 8 == 0) && (ldx % 8 == 0) && (x_sb % 8 == 0) &&
                    ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
   hipStream_t s = itts::as_stream(stream);
