@@ -217,6 +217,8 @@ def main():
                          "utterance), c5 (srt_dubbing long-form: a synthetic SRT of --cues cues sharded over the "
                          "ranks, length-bucketed chunks of 32 streamed through the pipelined driver)")
     ap.add_argument("--cues", type=int, default=256)
+    ap.add_argument("--chunk", type=int, default=128,
+                    help="C5: rows per decode chunk (the product's long-form chunk, IndexTTS.LONGFORM_BATCH)")
     ap.add_argument("--decoding", choices=("greedy", "beam3"), default="greedy",
                     help="greedy (the headline) or beam3: the reference's default production decoding "
                          "(do_sample=True, num_beams=3, top_k=30, top_p=0.8, infer.py:535-543), 3 beam rows "
@@ -387,7 +389,8 @@ def main():
 def long_form(args, cfg, gsd, vsd, dev, world, rank):
     """C5 (BASELINE.json configs[4]): srt_dubbing long-form.  A synthetic SRT of args.cues cues (seed 3),
     cue text L ~ U[8, 96], one shared prompt (features computed once, cached by key); cue i runs on rank
-    i % world; each rank sorts its cues by length into chunks of 32 (the decode ids padded to the chunk's
+    i % world; each rank sorts its cues by length into chunks of args.chunk (default 128, the product's
+    long-form chunk: IndexTTS.LONGFORM_BATCH; the decode ids padded to the chunk's
     bucket with the stop id 1 via ``pad_to`` -- prepare_gpt_inputs strips it, the latent pass gets the
     unpadded ids: per-cue results are unchanged), 6 codes per text token of the bucket (EOS
     suppressed), and streams the chunks through the pipelined driver;
@@ -404,8 +407,8 @@ def long_form(args, cfg, gsd, vsd, dev, world, rank):
     tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + 96 + 2 + 1 + 6 * 96 + 8)
     mine = sorted(shard(n_cues, world, rank), key=lambda i: -int(lens_all[i]))
     batches, keys, order = [], [], []
-    for c in range(0, len(mine), 32):
-        idx = mine[c: c + 32]
+    for c in range(0, len(mine), args.chunk):
+        idx = mine[c: c + args.chunk]
         order += idx
         bl = next(b for b in buckets if b >= max(int(lens_all[i]) for i in idx))
         tx = [texts_all[i].to(dev) for i in idx]
@@ -454,7 +457,7 @@ def long_form(args, cfg, gsd, vsd, dev, world, rank):
             "data": "synthetic: seeded random-init IndexTTS-1.5 weights, one random 511-frame prompt mel, "
                     "random cue text ids",
             "config": {"workload": f"C5: srt long-form, {n_cues} cues (L ~ U[8,96]) sharded over {world} GPU(s), "
-                                   "length-bucketed chunks of 32 (buckets 32/64/96 text ids, 6 codes per id: <= 600 = max_mel_tokens), "
+                                   f"length-bucketed chunks of {args.chunk} (buckets 32/64/96 text ids, 6 codes per id: <= 600 = max_mel_tokens), "
                                    "pipelined decode || latent+vocoder, RCCL gather",
                        "global_batch": n_cues, "seq_len": None, "parallelism": f"dp{world}"}}), flush=True)
     if world > 1:
