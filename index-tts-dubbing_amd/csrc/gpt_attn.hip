@@ -68,6 +68,12 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 // and arrive while the keys stream.  The 32 workgroups of one head land on one XCD (dispatch is
 // round-robin over XCDs and the grid is head-fastest), so each XCD's L2 holds only 2 heads' rows.
 // One kernel boundary and the separate c_proj launch less per layer.
+// K/V cache rows are read once per step: non-temporal loads (decode step 816 -> 792 us at C3 vs
+// plain loads; the weight stream stays non-temporal too, plain weight loads were slower:
+// profiles/nt_ab_r02.txt).  ITTS_KV_NT=0 builds the plain-load variant.
+#ifndef ITTS_KV_NT
+#define ITTS_KV_NT 1
+#endif
 template <typename TC, typename TO, int NT, bool ROWS, bool PROJ>
 __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
                                                          int64_t split_stride, const float* __restrict__ qkv_bias,
@@ -121,7 +127,14 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
     for (int u = 0; u < KB; ++u) {
       const int j = min(j0 + NG * u + g, max(nk - 2, 0));
 #pragma unroll
-      for (int w = 0; w < RW; ++w) dst[u][w] = reinterpret_cast<const u32x4_t*>(base + koff(p0 + j) + 8 * d8)[w];
+      for (int w = 0; w < RW; ++w) {
+        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(base + koff(p0 + j) + 8 * d8) + w;
+#if ITTS_KV_NT
+        dst[u][w] = __builtin_nontemporal_load(src);
+#else
+        dst[u][w] = *src;
+#endif
+      }
     }
   };
   kv_load(kr, Kc, 0);

@@ -44,6 +44,16 @@ __device__ __forceinline__ float wg_sum(float v, float* red) {
   return s;
 }
 
+// weight-stream loads of the decode GEMMs (A/B builds: ITTS_W_NT=0 uses plain loads)
+#ifndef ITTS_W_NT
+#define ITTS_W_NT 1
+#endif
+#if ITTS_W_NT
+#define ITTS_WLOAD(p) __builtin_nontemporal_load(p)
+#else
+#define ITTS_WLOAD(p) (*(p))
+#endif
+
 struct DgArgs {
   const void* a;      // LNMODE 0: bf16 A [.][lda]; else f32 X [.][lda]
   int64_t lda;
@@ -105,7 +115,7 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
   auto wload = [&](u32x4_t (&dst)[kU], int i0) {
 #pragma unroll
     for (int u = 0; u < kU; ++u)
-      if (i0 + u < niter) dst[u] = __builtin_nontemporal_load(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
+      if (i0 + u < niter) dst[u] = ITTS_WLOAD(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
   };
   wload(wa, 0);  // weight stream starts before the prologue
 
@@ -276,7 +286,7 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16_kernel(DgArgs p) {
   auto wload = [&](u32x4_t (&dst)[kU], int i0) {
 #pragma unroll
     for (int u = 0; u < kU; ++u)
-      if (i0 + u < niter) dst[u] = __builtin_nontemporal_load(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
+      if (i0 + u < niter) dst[u] = ITTS_WLOAD(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
   };
   wload(wa, 0);
   f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -383,7 +393,7 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
   auto wload = [&](u32x4_t (&dst)[kU], int i0) {
 #pragma unroll
     for (int u = 0; u < kU; ++u)
-      if (i0 + u < niter) dst[u] = __builtin_nontemporal_load(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
+      if (i0 + u < niter) dst[u] = ITTS_WLOAD(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
   };
   wload(wa, 0);
   f32x4_t acc[2 * MT];
