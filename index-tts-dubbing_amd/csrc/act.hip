@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p) {
     const int r = v / CV, c = (v - r * CV) * 8;
     if (v < WROWS * CV && r >= 1 && r <= TT + 12 && c0 + c < p.C) {
       const int t = min(max(t0 - 7 + r, 0), len - 1);
-      buf[i] = *reinterpret_cast<const u32x4_t*>(x + (int64_t)t * p.sxt + c0 + c);
+      buf[i] = ld_stream(reinterpret_cast<const u32x4_t*>(x + (int64_t)t * p.sxt + c0 + c));
     }
   }
 #pragma unroll

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
       if (v < XR * cv8) {
         const int r = v / cv8, c = (v - r * cv8) * 8;
         const int t = min(max(q0 - p.hl - 6 + r, 0), len - 1);
-        lv[i] = *reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c);
+        lv[i] = ld_stream(reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c));
       }
     }
 #pragma unroll
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
       if (v < WR * cv8) {
         const int r = v / cv8, c = (v - r * cv8) * 8;
         const int t = q0 - p.hl + r;
-        if (t >= 0 && t < len) lv[i] = *reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c);
+        if (t >= 0 && t < len) lv[i] = ld_stream(reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c));
       }
     }
 #pragma unroll
@@ -211,8 +211,8 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
     if (v < nvec) {
       const int e = v * 8, r = e / Cout, c = e - r * Cout;
       const int64_t off = (int64_t)r * p.ldy + c;
-      if (R1) rv1[i] = *reinterpret_cast<const u32x4_t*>(R1 + off);
-      if (R2) rv2[i] = *reinterpret_cast<const u32x4_t*>(R2 + off);
+      if (R1) rv1[i] = ld_stream(reinterpret_cast<const u32x4_t*>(R1 + off));
+      if (R2) rv2[i] = ld_stream(reinterpret_cast<const u32x4_t*>(R2 + off));
     }
   }
 

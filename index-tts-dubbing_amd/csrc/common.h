@@ -40,6 +40,20 @@ template <> struct St<_Float16> {
   __device__ __forceinline__ static void st(_Float16* p, float v) { *p = (_Float16)v; }
 };
 
+// Loads of data a kernel reads once (activation windows, residual rows, split-K partials): non-temporal
+// when ITTS_STREAM_NT (A/B builds; the K/V cache loads are non-temporal unconditionally, gpt_attn.hip)
+#ifndef ITTS_STREAM_NT
+#define ITTS_STREAM_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+#if ITTS_STREAM_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -112,7 +112,7 @@ __global__ __launch_bounds__(1024) void residual_reduce_ln_v4_kernel(
   f32x4_t bv = bias ? *reinterpret_cast<const f32x4_t*>(bias + e) : f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < kMaxSplit; ++s)
-    if (s < nsplit) pv[s] = *reinterpret_cast<const f32x4_t*>(part + s * split_stride + (int64_t)m * ldp + e);
+    if (s < nsplit) pv[s] = ld_stream(reinterpret_cast<const f32x4_t*>(part + s * split_stride + (int64_t)m * ldp + e));
   f32x4_t g1v = {0.f, 0.f, 0.f, 0.f}, b1v = g1v, g2v = g1v, b2v = g1v;
   if (g1) {
     g1v = *reinterpret_cast<const f32x4_t*>(g1 + e);
