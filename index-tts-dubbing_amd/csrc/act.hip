@@ -177,61 +177,73 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
 }
 
 // ---- bf16 channel-last path with both FIRs on MFMA (act_mfma.h) ----
-// Workgroup = 4 waves = NB 32-channel blocks x (4 / NB) strips of S output tiles (32 rows each):
-// TT = (4 / NB) * 32 * S output rows x NB * 32 channels.  The window [TT + 32 rows][NB * 64 B] holds
-// x rows t0 - 7 .. t0 + TT + 24 (rows the FIRs weight by zero are zero-filled, not loaded), replicate-
-// clamped per utterance.  Interior outputs leave straight from the down product's accumulators
-// (8-B stores of 4 channels); outputs within 3 samples of an utterance edge, where the down-sampler's
-// own replicate pad applies, are recomputed by the VALU formula from the same window.
+// Job = TT = (4 / NB) * 32 * S output rows x NB * 32 channels of one utterance; a workgroup (4 waves
+// = NB 32-channel blocks x (4 / NB) strips of S 32-row tiles) keeps one channel group and walks jobs
+// blockIdx.y, + gridDim.y, ... (persistent): the taps and channel constants are built once, and the
+// next job's window loads are in flight while this job's strips compute.  The window [TT + 32
+// rows][NB * 64 B] holds x rows t0 - 7 .. t0 + TT + 24 (rows the FIRs weight by zero are zero, not
+// loaded), replicate-clamped per utterance.  Interior outputs leave straight from the down product's
+// accumulators (8-B stores of 4 channels); outputs within 3 samples of an utterance edge, where the
+// down-sampler's own replicate pad applies, are recomputed by the VALU formula from the same window.
 template <int NB, int S>
-__global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p) {
+__global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p, int ntt, int njobs) {
   constexpr int PX = NB * 64, NS = 4 / NB, TT = NS * 32 * S, WROWS = TT + 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char win[];
-  const int b = blockIdx.z;
-  const int len = p.lens ? p.lens[b] : p.T;
-  const int t0 = blockIdx.y * TT;
-  if (t0 >= len) return;
   const int c0 = blockIdx.x * NB * 32;
-  const uint16_t* x = reinterpret_cast<const uint16_t*>(p.x) + (int64_t)b * p.sxb;
-  uint16_t* y = reinterpret_cast<uint16_t*>(p.y) + (int64_t)b * p.syb;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-  // ---- window: rows 1 .. TT + 12 (t0 - 6 .. t0 + TT + 5) loaded, the rest zero ----
   constexpr int CV = NB * 4;  // 16-B vectors per row
   constexpr int NV = (WROWS * CV + 255) / 256;
-  u32x4_t buf[NV];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int v = tid + 256 * i;
-    buf[i] = u32x4_t{0u, 0u, 0u, 0u};
-    const int r = v / CV, c = (v - r * CV) * 8;
-    if (v < WROWS * CV && r >= 1 && r <= TT + 12 && c0 + c < p.C) {
-      const int t = min(max(t0 - 7 + r, 0), len - 1);
-      buf[i] = ld_stream(reinterpret_cast<const u32x4_t*>(x + (int64_t)t * p.sxt + c0 + c));
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int v = tid + 256 * i;
-    const int r = v / CV, c = (v - r * CV) * 8;
-    if (v < WROWS * CV) *reinterpret_cast<u32x4_t*>(win + itts_actm::woff<PX>(r, c)) = buf[i];
-  }
   float* tl = reinterpret_cast<float*>(win + WROWS * PX);  // 12 up taps, 12 down taps
   if (tid < 24) tl[tid] = tid < 12 ? p.up[tid] : p.down[tid - 12];
-  __syncthreads();
 
-  // ---- strips ----
+  // window rows 1 .. TT + 12 (t0 - 6 .. t0 + TT + 5) of job j into registers
+  u32x4_t buf[NV];
+  auto wload = [&](int j) {
+    const int b = j / ntt, t0 = (j - b * ntt) * TT;
+    const int len = p.lens ? p.lens[b] : p.T;
+    const uint16_t* x = reinterpret_cast<const uint16_t*>(p.x) + (int64_t)b * p.sxb;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + 256 * i;
+      buf[i] = u32x4_t{0u, 0u, 0u, 0u};
+      const int r = v / CV, c = (v - r * CV) * 8;
+      if (t0 < len && v < WROWS * CV && r >= 1 && r <= TT + 12 && c0 + c < p.C) {
+        const int t = min(max(t0 - 7 + r, 0), len - 1);
+        buf[i] = ld_stream(reinterpret_cast<const u32x4_t*>(x + (int64_t)t * p.sxt + c0 + c));
+      }
+    }
+  };
+  int job = blockIdx.y;
+  if (job < njobs) wload(job);
+  __syncthreads();  // taps staged
+
   const int blk = wave % NB, sidx = wave / NB;
-  const int cb = 32 * blk;                 // window column of the block
-  const int ts = t0 + sidx * 32 * S;       // first output of the strip
-  const int ntile = min(S, max(0, (len - ts + 31) / 32));
-  {
-    itts_actm::Taps T;
-    itts_actm::make_taps(tl, T);
-    const int ch = c0 + cb + (lane & 31);
-    const float a_rev = ch < p.C ? expf(p.log_alpha[ch]) * 0.15915494309189535f : 0.f;
-    const float inv_b = ch < p.C ? 1.0f / (expf(p.log_beta[ch]) + 1e-9f) : 0.f;
-    const int h = lane >> 5;
+  const int cb = 32 * blk;  // window column of the block
+  itts_actm::Taps T;
+  itts_actm::make_taps(tl, T);
+  const int ch = c0 + cb + (lane & 31);
+  const float a_rev = ch < p.C ? expf(p.log_alpha[ch]) * 0.15915494309189535f : 0.f;
+  const float inv_b = ch < p.C ? 1.0f / (expf(p.log_beta[ch]) + 1e-9f) : 0.f;
+  const int h = lane >> 5;
+
+  for (; job < njobs; job += gridDim.y) {
+    const int b = job / ntt, t0 = (job - b * ntt) * TT;
+    const int len = p.lens ? p.lens[b] : p.T;
+    __syncthreads();  // the previous job's readers of the window are done
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + 256 * i;
+      const int r = v / CV, c = (v - r * CV) * 8;
+      if (v < WROWS * CV) *reinterpret_cast<u32x4_t*>(win + itts_actm::woff<PX>(r, c)) = buf[i];
+    }
+    __syncthreads();
+    if (job + gridDim.y < njobs) wload(job + gridDim.y);  // in flight during this job's strips
+    if (t0 >= len) continue;  // uniform per workgroup
+    uint16_t* y = reinterpret_cast<uint16_t*>(p.y) + (int64_t)b * p.syb;
+
+    // ---- strips ----
+    const int ts = t0 + sidx * 32 * S;  // first output of the strip
+    const int ntile = min(S, max(0, (len - ts + 31) / 32));
     itts_actm::strip<PX>(win, sidx * 32 * S, cb, ntile, T, a_rev, inv_b, [&](int i, const f32x16_t& acc) {
       const int t = ts + 32 * i + (lane & 31);
       if (t < 3 || t >= len - 3) return;  // edges: VALU fix-up below
@@ -244,29 +256,34 @@ __global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p) {
         }
       }
     });
-  }
 
-  // ---- outputs within 3 samples of an utterance edge (uniform per block) ----
-  if (t0 < 3 || t0 + TT > len - 3) {
-    const int te = min(t0 + TT, len);
-    for (int it = tid; it < 6 * NB * 32; it += 256) {
-      const int e = it / (NB * 32), cc = it - e * (NB * 32);
-      const int t = e < 3 ? e : len - 6 + e;
-      if (t < t0 || t >= te || t < 0 || (e >= 3 && t < 3) || c0 + cc >= p.C) continue;
-      const float a = expf(p.log_alpha[c0 + cc]) * 0.15915494309189535f;
-      const float inv_b = 1.0f / (expf(p.log_beta[c0 + cc]) + 1e-9f);
-      y[(int64_t)t * p.syt + c0 + cc] = f2bf(itts_actm::exact_at<PX>(win, t0 - 7, t, len, cc, tl, a, inv_b));
+    // ---- outputs within 3 samples of an utterance edge (uniform per block) ----
+    if (t0 < 3 || t0 + TT > len - 3) {
+      const int te = min(t0 + TT, len);
+      for (int it = tid; it < 6 * NB * 32; it += 256) {
+        const int e = it / (NB * 32), cc = it - e * (NB * 32);
+        const int t = e < 3 ? e : len - 6 + e;
+        if (t < t0 || t >= te || t < 0 || (e >= 3 && t < 3) || c0 + cc >= p.C) continue;
+        const float a = expf(p.log_alpha[c0 + cc]) * 0.15915494309189535f;
+        const float ib = 1.0f / (expf(p.log_beta[c0 + cc]) + 1e-9f);
+        y[(int64_t)t * p.syt + c0 + cc] = f2bf(itts_actm::exact_at<PX>(win, t0 - 7, t, len, cc, tl, a, ib));
+      }
     }
   }
 }
 
+#ifndef ITTS_ACT_WGS  // resident workgroups targeted by the persistent activation grid
+#define ITTS_ACT_WGS 512
+#endif
 template <int NB, int S>
 void launch_mfma(const ActArgs& a, hipStream_t s) {
   constexpr int TT = (4 / NB) * 32 * S;
-  const int nblk = (a.C + 31) / 32;
-  dim3 grid((nblk + NB - 1) / NB, (a.T + TT - 1) / TT, a.B);
+  const int nblk = (a.C + 31) / 32, ngrp = (nblk + NB - 1) / NB;
+  const int ntt = (a.T + TT - 1) / TT, njobs = ntt * a.B;
+  int per = ITTS_ACT_WGS / ngrp;
+  per = per < 1 ? 1 : (per > njobs ? njobs : per);
   const size_t lds = (size_t)(TT + 32) * NB * 64 + 24 * sizeof(float);
-  hipLaunchKernelGGL((aa_snake_mfma_kernel<NB, S>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((aa_snake_mfma_kernel<NB, S>), dim3(ngrp, per, 1), dim3(256), lds, s, a, ntt, njobs);
 }
 
 template <typename TI, typename TO>
