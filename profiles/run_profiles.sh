@@ -29,7 +29,7 @@ if [ "${2:-pmc}" = "pmc" ]; then
       -d /tmp/pmc_vsq -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vsq.log 2>&1
   timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES --output-format csv \
       -d /tmp/pmc_vsi -o run -- python3 profiles/pmc_vocoder.py > gpurun_out/pmc_vsi.log 2>&1
-  { python3 profiles/pmc_summary.py /tmp/pmc_vsq amp_conv aa_snakebeta igemm;
-    python3 profiles/pmc_summary.py /tmp/pmc_vsi amp_conv aa_snakebeta igemm; } > gpurun_out/pmc_sq_vocoder_$TAG.txt
+  { python3 profiles/pmc_summary.py /tmp/pmc_vsq amp_conv aa_snake igemm;
+    python3 profiles/pmc_summary.py /tmp/pmc_vsi amp_conv aa_snake igemm; } > gpurun_out/pmc_sq_vocoder_$TAG.txt
 fi
 echo profiles-done

@@ -40,7 +40,8 @@ def load(d, counter):
 
 
 def short(name):
-    for k in sorted(DECODE_KERNELS, key=len, reverse=True) + ["igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel"]:
+    for k in sorted(DECODE_KERNELS, key=len, reverse=True) + ["igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel",
+                                                              "aa_snake_mfma_kernel"]:
         if k in name:
             return k
     return name.split("(")[0][-40:]
@@ -50,7 +51,8 @@ def vocoder(fetch, write):
     out = {"kernel": "igemm_kernel (BigVGAN convs, second of two C3 vocoder forwards)"}
     groups = {"igemm_kernel": lambda n: "igemm_kernel" in n,
               "amp_conv_kernel": lambda n: bool(re.search(r"amp_conv_kernel<[^>]*true>", n)),  # act fused
-              "aa_snakebeta_kernel": lambda n: "aa_snakebeta_kernel" in n}
+              # the activation: MFMA kernel on the vocoder's bf16 channel-last layout (VALU kernel otherwise)
+              "aa_snakebeta_kernel": lambda n: "aa_snakebeta_kernel" in n or "aa_snake_mfma_kernel" in n}
     for name, match in groups.items():
         ids = sorted(k for k, (n, _) in fetch.items() if match(n) and k in write)
         ids = ids[len(ids) // 2:]
