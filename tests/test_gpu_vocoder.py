@@ -108,6 +108,38 @@ def test_activation_kernel_bf16_mfma_path_vs_f32_path(C):
     assert float(same) > 0.6, float(same)
 
 
+@pytest.mark.parametrize("C,B,T", [(24, 160, 3000), (768, 64, 700), (192, 48, 1500)])
+def test_activation_kernel_mfma_persistent_many_jobs(C, B, T):
+    """The MFMA activation kernel is persistent (each workgroup walks several (utterance, time tile)
+    jobs with the next window's loads in flight): shapes with more jobs than resident workgroups and
+    ragged lengths (incl. empty tiles, a 1-sample and a 5-sample row) vs the f32 VALU path, same
+    bound as above."""
+    from indextts.utils.synthetic import kaiser_sinc_lowpass
+    _hip, lib = _lib()
+    g = torch.Generator().manual_seed(C + B)
+    lens = torch.randint(1, T + 1, (B,), generator=g, dtype=torch.int32)
+    lens[0], lens[1], lens[2] = T, 1, 5
+    x = (torch.randn(B, T, C, generator=g) * 1.5).to(torch.bfloat16).cuda()
+    f = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).cuda()
+    la, lb = (torch.randn(C, generator=g) * 0.5).cuda(), (torch.randn(C, generator=g) * 0.5).cuda()
+    lensd = lens.cuda()
+    sentinel = -12352.0
+    yb = torch.full((B, T, C), sentinel, dtype=torch.bfloat16, device="cuda")
+    yf = torch.full((B, T, C), sentinel, dtype=torch.float32, device="cuda")
+    for xin, yout, dt in ((x, yb, _hip.BF16), (x.float(), yf, _hip.F32)):
+        _hip.check(lib.itts_aa_snakebeta_fwd(xin.data_ptr(), yout.data_ptr(), f.data_ptr(), f.data_ptr(),
+                                             la.data_ptr(), lb.data_ptr(), lensd.data_ptr(), B, C, T, T * C, C, 1,
+                                             T * C, C, 1, dt, dt, _hip.stream_ptr()), "fwd")
+    torch.cuda.synchronize()
+    yb, yf = yb.cpu(), yf.cpu()
+    rms = float(yf[0].pow(2).mean().sqrt())
+    for b in range(B):
+        L = int(lens[b])
+        err = (yb[b, :L].float() - yf[b, :L]).abs()
+        assert bool((err <= 2.0 ** -7 * yf[b, :L].abs() + 5e-3 * rms).all()), b
+        assert bool((yb[b, L:].float() == sentinel).all()), b
+
+
 @pytest.mark.parametrize("i", range(5))
 def test_activation_kernel_f16_bct(golden, i):
     """f16 in / f16 out through the reference op's argument list (the extension dispatches Half too,
