@@ -607,25 +607,36 @@ class HipGPT:
         ev = self.step_events  # optional instrumentation: HIP events around each lane's step
         keys0 = [int((r1 - r0) * (s + 2)) - int(pad[r0:r1].sum()) for r0, r1 in self._lane_bounds(B, lanes)] \
             if ev is not None else None
+        kmulti = self.GRAPH_STEPS if (len(work) == 1 and trace is None and work[0]["graph_ok"]) else 1
         while steps < max_new_tokens:
+            # kmulti decode steps per graph replay (one captured graph holds kmulti steps) while whole
+            # groups fit before max_new_tokens and inside one done-check interval
+            n = kmulti if (kmulti > 1 and steps + kmulti <= max_new_tokens
+                           and (steps % check_every) + kmulti <= check_every) else 1
             for li, ln in enumerate(work):
                 with torch.cuda.stream(ln["stream"]):
                     if ev is not None:
                         e0 = torch.cuda.Event(enable_timing=True)
                         e0.record()
-                    if ln["graph_ok"]:
+                    if n > 1:
+                        self._multi_graph(ln, n, min_new_tokens, repetition_penalty, gkey).replay()
+                    elif ln["graph_ok"]:
                         ln["graph"][0].replay()
                     else:
                         self._decode_step(ln["st"], min_new_tokens, repetition_penalty)
                     if ev is not None:
                         e1 = torch.cuda.Event(enable_timing=True)
                         e1.record()
-                        # keys attended this step, summed over the lane's rows: s + 2 + r - pad_b
-                        ev.append((e0, e1, ln["st"]["B"], keys0[li] + ln["st"]["B"] * (steps - 1)))
+                        # keys attended per step, summed over the lane's rows: s + 2 + r - pad_b (a
+                        # multi-step replay: its interval once, then zero-length entries per extra step)
+                        for j in range(n):
+                            ev.append((e0 if j == 0 else e1, e1, ln["st"]["B"],
+                                       keys0[li] + ln["st"]["B"] * (steps - 1 + j)))
                     if trace is not None:
                         trace.append(ln["st"]["logits"][:, : self.V].clone())
-            steps += 1
-            if steps % check_every == 0:
+            prev = steps
+            steps += n
+            if steps // check_every != prev // check_every:
                 done = True
                 for ln in work:
                     with torch.cuda.stream(ln["stream"]):
@@ -691,6 +702,27 @@ class HipGPT:
     MUTABLE = ("t", "x", "h", "seen", "done", "codes")
     BEAM_MUTABLE = ("beam_score", "kv_rows", "done_u", "hyp_score", "hyp_len", "hyp_codes", "hyp_n", "hyp_order",
                     "hyp_worst")
+
+    # decode steps per captured graph replay (ITTS_GRAPH_STEPS; 1 = one step per replay): 4 steps
+    # per graph 776 vs 785 us per step (profiles/graph_steps_r02.txt: the boundary between two graph
+    # launches costs more than a kernel boundary inside one graph)
+    GRAPH_STEPS = int(os.environ.get("ITTS_GRAPH_STEPS", "4"))
+
+    def _multi_graph(self, ln, n, min_new, penalty, gkey):
+        """the lane's n-step graph (captured on first use, like the one-step graph)."""
+        mg = ln.get("multi")
+        if mg is None or mg[1] != (n, gkey):
+            st = ln["st"]
+            keys = self.MUTABLE + (self.BEAM_MUTABLE if "kv_rows" in st else ())
+            saved = {k: st[k].clone() for k in keys}
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    self._decode_step(st, min_new, penalty)
+            for k, v in saved.items():
+                st[k].copy_(v)
+            mg = ln["multi"] = (g, (n, gkey))
+        return mg[0]
 
     def _capture(self, st, min_new, penalty):
         """Capture one decode step into a hipGraph; counters are device-side so replays advance."""
