@@ -860,20 +860,27 @@ class HipGPT:
         # distinct cache keys a step reads: each utterance's prompt once (shared by its beams through
         # the lineage table) + every beam row's generated keys
         keys0 = int(B * (s + 1) - int(pad.sum())) if ev is not None else 0
+        kmulti = self.GRAPH_STEPS if graph_ok else 1
         while steps < max_new_tokens:
+            n = kmulti if (kmulti > 1 and steps + kmulti <= max_new_tokens
+                           and (steps % check_every) + kmulti <= check_every) else 1
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            if graph_ok:
+            if n > 1:
+                self._multi_graph(ln, n, min_new_tokens, repetition_penalty, gkey).replay()
+            elif graph_ok:
                 ln["graph"][0].replay()
             else:
                 self._decode_step(st, min_new_tokens, repetition_penalty)
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
-                ev.append((e0, e1, R, keys0 + R * steps))
-            steps += 1
-            if steps % check_every == 0 and bool(st["done_u"].all()):
+                for j in range(n):
+                    ev.append((e0 if j == 0 else e1, e1, R, keys0 + R * (steps + j)))
+            prev = steps
+            steps += n
+            if steps // check_every != prev // check_every and bool(st["done_u"].all()):
                 break
         return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
 
