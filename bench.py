@@ -85,9 +85,10 @@ def install_conv_timer(voc, timer):
 
 
 def install_hbm_timers(voc, t_act, t_amp):
-    """HIP events around the standalone activation launches and the fused act+conv launches (C = 24 /
-    48), with their algorithmic HBM bytes: valid rows x channels, each element read once and written
-    once (+ residual rows read; + the packed weights once)."""
+    """HIP events around the standalone activation launches and the AMPBlock1 conv launches
+    (itts_amp_conv_fwd, C = 24 / 48 / 96, conv-only or with the activation fused), with their
+    algorithmic HBM bytes: valid rows x channels, each element read once and written once
+    (+ residual rows read; + the packed weights once)."""
     orig_act, orig_amp = voc._act, voc._amp
 
     def act(a, x, y, lens):
@@ -95,8 +96,6 @@ def install_hbm_timers(voc, t_act, t_amp):
         return t_act.wrap(lambda: orig_act(a, x, y, lens), 0.0, nbytes)
 
     def amp(c, x, y, lens, a=None, r1=None, r2=None, alpha=1.0):
-        if a is None:  # conv-only variant (C = 96): not the HBM-bound fused kernel
-            return orig_amp(c, x, y, lens, a, r1, r2, alpha)
         nres = (r1 is not None) + (r2 is not None)
         nbytes = 2.0 * voc.rows * (c.cin + c.cout * (1 + nres)) + 2.0 * c.ntaps * c.cin * c.cout
         return t_amp.wrap(lambda: orig_amp(c, x, y, lens, a, r1, r2, alpha), 2.0 * voc.rows * c.cout * c.cin * c.ntaps,
@@ -343,10 +342,10 @@ def main():
            "algorithmic_bytes_per_launch": round(timer.bytes / max(k_n, 1)),
            "share_of_step": round(k_ms / (1e3 * dt / args.steps), 3)}
     hbm = {}
-    for key, t, name, tkey in (("roofline_vocoder_act", t_act, "itts_aa_snakebeta_fwd (Activation1d, C >= 96 stages "
-                                "and activation_post)", "aa_snakebeta_bytes_per_launch"),
-                               ("roofline_vocoder_amp", t_amp, "itts_amp_conv_fwd (Activation1d fused into the "
-                                "AMPBlock1 convs, C = 24 / 48)", "amp_conv_bytes_per_launch")):
+    for key, t, name, tkey in (("roofline_vocoder_act", t_act, "itts_aa_snakebeta_fwd (Activation1d, every AMP "
+                                "stage and activation_post)", "aa_snakebeta_bytes_per_launch"),
+                               ("roofline_vocoder_amp", t_amp, "itts_amp_conv_fwd (AMPBlock1 dilated convs "
+                                "+ residuals, C = 24 / 48 / 96)", "amp_conv_bytes_per_launch")):
         ms, _, n = t.result()
         if n:
             gbs = t.bytes / (ms * 1e-3) / 1e9

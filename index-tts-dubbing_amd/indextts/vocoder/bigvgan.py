@@ -116,14 +116,16 @@ class _Act:
 
 
 class HipBigVGAN:
-    # AMP stage kernels by channel count (measured per conv on MI355X, B=32 x 400 frames):
-    #   24, 48: act fused into itts_amp_conv_fwd;  96: act kernel + itts_amp_conv_fwd without act
-    #   (the fused form ties the igemm path there, the split form beats both);  others: act + igemm
-    FUSED_CHANNELS = (24, 48)
-    SPLIT_CHANNELS = (96,)
+    # AMP stage kernels by channel count (measured per conv on MI355X, B=32 x 400 frames,
+    # profiles/amp_ab_r02.txt): 24, 48, 96: the MFMA activation kernel + itts_amp_conv_fwd without
+    # act (vocoder 101 ms; act fused into the conv for 24 / 48: 107 ms);  others: act + igemm
+    FUSED_CHANNELS = ()
+    SPLIT_CHANNELS = (24, 48, 96)
     if os.environ.get("ITTS_VOC_FUSED") is not None:  # tuning sweeps: "24,48,96"
         FUSED_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_FUSED"].split(",") if v)
         SPLIT_CHANNELS = tuple(sorted({24, 48, 96} - set(FUSED_CHANNELS)))
+    if os.environ.get("ITTS_VOC_SPLIT") is not None:  # channel counts not listed in either: igemm
+        SPLIT_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_SPLIT"].split(",") if v)
 
     def __init__(self, state_dict, cfg_bv, device="cuda"):
         self.lib = _hip.load()
