@@ -33,6 +33,9 @@ constexpr int kMaxTapsAc = 16;
 #ifndef ITTS_AMP_TT96
 #define ITTS_AMP_TT96 128
 #endif
+#ifndef ITTS_AMP_K48  // K extent of the C = 48 instantiation (48: no all-zero K chunk)
+#define ITTS_AMP_K48 48
+#endif
 #ifndef ITTS_AMP_TTC32  // conv-only (activation in its own kernel)
 #define ITTS_AMP_TTC32 ITTS_AMP_TT32
 #endif
@@ -41,12 +44,6 @@ constexpr int kMaxTapsAc = 16;
 #endif
 #ifndef ITTS_AMP_TTC96
 #define ITTS_AMP_TTC96 ITTS_AMP_TT96
-#endif
-#ifndef ITTS_AMP_WDIRECT
-#define ITTS_AMP_WDIRECT 0
-#endif
-#ifndef ITTS_AMP_LATE_RES
-#define ITTS_AMP_LATE_RES 0
 #endif
 constexpr int kSpan = 64;  // max (max_off - min_off) of the taps
 
@@ -75,8 +72,11 @@ __device__ __forceinline__ float snake_f(float u, float a_rev, float inv_b) {
 __device__ __forceinline__ float ld_bf(const uint16_t* p) { return __uint_as_float(((uint32_t)*p) << 16); }
 
 // CK: the channel count (Cin == Cout) as a compile-time constant for the BigVGAN stages, 0 = runtime
+// CIN_PAD: the K extent staged and multiplied (a multiple of 16 >= Cin); the packed weights' rows
+// are WS = CIN_PAD rounded up to 32 wide (the igemm packing)
 template <int CIN_PAD, int COUT_PAD, int TT, bool ACT, int CK>
-__global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
+__device__ __forceinline__ void amp_conv_body(const AcArgs& p) {
+  constexpr int WS = (CIN_PAD + 31) / 32 * 32;
   constexpr int PA = CIN_PAD * 2 + 16;  // activated-window row pitch (bytes)
   constexpr int FN = COUT_PAD / 32, KS = CIN_PAD / 16, FM = TT / 128;
   constexpr int SR = 16;                // activation rows per work item
@@ -212,14 +212,13 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   }
 
   // residual rows of this tile: loads issued now, consumed in the epilogue (latency hidden by the MFMAs)
-  constexpr int kEV = (TT * COUT_PAD / 8 + 255) / 256;
+  constexpr int kEV = (TT * (CK ? CK : COUT_PAD) / 8 + 255) / 256;
   const int rows = min(TT, len - q0);
   const int nvec = rows * Cout / 8;
   uint16_t* Y = p.y + (int64_t)b * p.syb + (int64_t)q0 * p.ldy;
   const uint16_t* R1 = p.r1 ? p.r1 + (int64_t)b * p.syb + (int64_t)q0 * p.ldy : nullptr;
   const uint16_t* R2 = p.r2 ? p.r2 + (int64_t)b * p.syb + (int64_t)q0 * p.ldy : nullptr;
   u32x4_t rv1[kEV], rv2[kEV];
-  auto rload = [&] {
   // clamped unconditional loads (see the window loads); lanes past nvec do not store
   if (R1) {
 #pragma unroll
@@ -235,65 +234,11 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
       rv2[i] = ld_stream(reinterpret_cast<const u32x4_t*>(R2 + (int64_t)r * p.ldy + c));
     }
   }
-  };
-  if (!ITTS_AMP_LATE_RES) rload();
 
   // ---- 3. MFMA over taps x K chunks; wave w owns output rows [32(w + 4i), +32), i < FM ----
   // The tap weights go through a 2-slot LDS ring filled cooperatively by the whole workgroup (each
   // weight byte crosses L2 -> CU once per block, not once per wave), next tap's loads in flight
   // while this tap's MFMAs run; B fragments are then conflict-free ds_read_b128.
-#if ITTS_AMP_WDIRECT
-  // B fragments straight from global memory per wave (the packed weights stay L1/L2-resident),
-  // next tap's fragments in flight while this tap's MFMAs run; no barrier inside the tap loop
-  const int r32 = lane & 31, h = lane >> 5;
-  f32x16_t acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int n = 0; n < FN; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][n][r] = 0.f;
-  bf16x8_t bc[KS][FN];
-#if ITTS_AMP_WDIRECT == 2
-  bf16x8_t bn[KS][FN];
-#endif
-  auto bload = [&](int j, bf16x8_t (&dst)[KS][FN]) {
-    const uint16_t* Wj = p.w + (int64_t)j * COUT_PAD * CIN_PAD + r32 * CIN_PAD + h * 8;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int n = 0; n < FN; ++n)
-        dst[ks][n] = *reinterpret_cast<const bf16x8_t*>(Wj + 32 * n * CIN_PAD + ks * 16);
-  };
-#if ITTS_AMP_WDIRECT == 2
-  bload(0, bc);
-#endif
-  for (int j = 0; j < p.ntaps; ++j) {
-#if ITTS_AMP_WDIRECT == 2
-    if (j + 1 < p.ntaps) bload(j + 1, bn);
-#else
-    bload(j, bc);
-#endif
-    const int roff = r32 + p.tap_off[j] + p.hl;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(Aw + (32 * (wave + 4 * i) + roff) * PA + h * 16 + ks * 32);
-#pragma unroll
-        for (int n = 0; n < FN; ++n)
-          acc[i][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bc[ks][n], acc[i][n], 0, 0, 0);
-      }
-    }
-#if ITTS_AMP_WDIRECT == 2
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int n = 0; n < FN; ++n) bc[ks][n] = bn[ks][n];
-#endif
-  }
-  __syncthreads();  // the f32 output tile overlays the window
-#else
   constexpr int PW = CIN_PAD * 2 + 16;                   // ring row pitch (bytes)
   constexpr int WV = COUT_PAD * CIN_PAD / 8;             // 16-B vectors per tap
   constexpr int kWV = (WV + 255) / 256;                  // per thread
@@ -308,11 +253,12 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
       for (int r = 0; r < 16; ++r) acc[i][n][r] = 0.f;
   u32x4_t wv[kWV];
   auto wload = [&](int j) {
-    const uint16_t* Wj = p.w + (int64_t)j * COUT_PAD * CIN_PAD;
+    const uint16_t* Wj = p.w + (int64_t)j * COUT_PAD * WS;
 #pragma unroll
     for (int i = 0; i < kWV; ++i) {
-      const int v = tid + 256 * i;
-      if (v < WV) wv[i] = reinterpret_cast<const u32x4_t*>(Wj)[v];
+      const int v = min(tid + 256 * i, WV - 1);
+      const int n = v / (CIN_PAD / 8), c = (v - n * (CIN_PAD / 8)) * 8;
+      wv[i] = *reinterpret_cast<const u32x4_t*>(Wj + n * WS + c);
     }
   };
   auto wstore = [&](int slot) {
@@ -329,7 +275,6 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   wload(0);
   wstore(0);  // the raw window is consumed: the activation phase ended with a barrier
   __syncthreads();
-#pragma unroll 1  // unrolled copies of a small tap body hold several taps' weight loads (VGPRs, occupancy)
   for (int j = 0; j < p.ntaps; ++j) {
     if (j + 1 < p.ntaps) wload(j + 1);
     const unsigned char* wsl = Wr + (j & 1) * COUT_PAD * PW;
@@ -350,11 +295,9 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
     if (j + 1 < p.ntaps) wstore((j + 1) & 1);  // slot last read in tap j-1, fenced by its barrier
     __syncthreads();
   }
-#endif
 
   // ---- 4. epilogue: acc -> LDS f32 tile [TT][Cout] (overlays the window + ring) -> bias /
   //         residuals / alpha -> 16-B stores ----
-  if (ITTS_AMP_LATE_RES) rload();
   float* Ys = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -397,30 +340,45 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
   }
 }
 
+template <int CIN_PAD, int COUT_PAD, int TT, bool ACT, int CK>
+__global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
+  amp_conv_body<CIN_PAD, COUT_PAD, TT, ACT, CK>(p);
+}
+
+// the same with the register budget of 3 waves per SIMD, for instantiations whose LDS allows 3
+// workgroups per CU
+template <int CIN_PAD, int COUT_PAD, int TT, bool ACT, int CK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void amp_conv_kernel_w3(AcArgs p) {
+  amp_conv_body<CIN_PAD, COUT_PAD, TT, ACT, CK>(p);
+}
+
 template <int CI, int CO, int TT, bool ACT, int CK>
 void launch_one(const AcArgs& a, hipStream_t s) {
   constexpr int PA = CI * 2 + 16;
   const int WR = TT + a.hl + a.hr;
   const size_t raw = ACT ? (size_t)(WR + 12) * a.Cin * 2 : 0;
-  const size_t ring = ITTS_AMP_WDIRECT ? 0 : (size_t)2 * CO * (CI * 2 + 16);
+  const size_t ring = (size_t)2 * CO * (CI * 2 + 16);
   const size_t win = (size_t)(TT + kSpan) * PA;
   const size_t out = (size_t)TT * a.Cout * 4;  // overlays window + ring after the MFMAs
   size_t lds = win + (raw > ring ? raw : ring);
   if (lds < out) lds = out;
   dim3 grid((a.Tmax + TT - 1) / TT, 1, a.B);
-  hipLaunchKernelGGL((amp_conv_kernel<CI, CO, TT, ACT, CK>), grid, dim3(256), lds, s, a);
+  if constexpr (!ACT && CK == 48 && CI == 48)
+    hipLaunchKernelGGL((amp_conv_kernel_w3<CI, CO, TT, ACT, CK>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((amp_conv_kernel<CI, CO, TT, ACT, CK>), grid, dim3(256), lds, s, a);
 }
 
 // TTA / TTC: output rows per workgroup with / without the fused activation; CKN: the stage's channel
-// count that gets the compile-time-channel instantiation
-template <int CI, int CO, int TTA, int TTC, int CKN>
+// count that gets the compile-time-channel instantiation, with K extent CIK (a multiple of 16)
+template <int CI, int CO, int TTA, int TTC, int CKN, int CIK>
 void launch_ac(const AcArgs& a, hipStream_t s) {
   const bool ck = a.Cin == CKN && a.Cout == CKN;
   if (a.log_alpha) {
-    if (ck) launch_one<CI, CO, TTA, true, CKN>(a, s);
+    if (ck) launch_one<CIK, CO, TTA, true, CKN>(a, s);
     else launch_one<CI, CO, TTA, true, 0>(a, s);
   } else {
-    if (ck) launch_one<CI, CO, TTC, false, CKN>(a, s);
+    if (ck) launch_one<CIK, CO, TTC, false, CKN>(a, s);
     else launch_one<CI, CO, TTC, false, 0>(a, s);
   }
 }
@@ -476,9 +434,9 @@ extern "C" int itts_amp_conv_fwd(const void* x, int64_t x_sb, int64_t ldx, const
   ITTS_REQUIRE(hi - lo <= kSpan, fn, "tap span exceeds 64 rows");
   hipStream_t s = itts::as_stream(stream);
   const int ci = (Cin + 31) / 32 * 32, co = (Cout + 31) / 32 * 32;
-  if (ci == 32 && co == 32) launch_ac<32, 32, ITTS_AMP_TT32, ITTS_AMP_TTC32, 24>(a, s);
-  else if (ci == 64 && co == 64) launch_ac<64, 64, ITTS_AMP_TT64, ITTS_AMP_TTC64, 48>(a, s);
-  else if (ci == 96 && co == 96) launch_ac<96, 96, ITTS_AMP_TT96, ITTS_AMP_TTC96, 96>(a, s);
+  if (ci == 32 && co == 32) launch_ac<32, 32, ITTS_AMP_TT32, ITTS_AMP_TTC32, 24, 32>(a, s);
+  else if (ci == 64 && co == 64) launch_ac<64, 64, ITTS_AMP_TT64, ITTS_AMP_TTC64, 48, ITTS_AMP_K48>(a, s);
+  else if (ci == 96 && co == 96) launch_ac<96, 96, ITTS_AMP_TT96, ITTS_AMP_TTC96, 96, 96>(a, s);
   else return itts::fail(fn, "supported (Cin, Cout) padded pairs: (32,32), (64,64), (96,96)");
   return itts::check_launch(fn);
 }
