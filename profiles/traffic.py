@@ -50,7 +50,7 @@ def short(name):
 def vocoder(fetch, write):
     out = {"kernel": "igemm_kernel (BigVGAN convs, second of two C3 vocoder forwards)"}
     groups = {"igemm_kernel": lambda n: "igemm_kernel" in n,
-              "amp_conv_kernel": lambda n: bool(re.search(r"amp_conv_kernel<[^>]*true>", n)),  # act fused
+              "amp_conv_kernel": lambda n: "amp_conv_kernel" in n,  # conv-only and act-fused forms
               # the activation: MFMA kernel on the vocoder's bf16 channel-last layout (VALU kernel otherwise)
               "aa_snakebeta_kernel": lambda n: "aa_snakebeta_kernel" in n or "aa_snake_mfma_kernel" in n}
     for name, match in groups.items():
