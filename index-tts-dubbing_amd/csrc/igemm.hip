@@ -28,6 +28,9 @@ namespace {
 
 constexpr int kMaxTaps = 16;
 constexpr int kWinSpan = 64;  // WIN: max tap span (rows)
+#ifndef ITTS_IG_WIN_MINTAPS  // fewest taps that take the window form
+#define ITTS_IG_WIN_MINTAPS 5
+#endif
 
 struct IgArgs {
   const uint16_t* x;
@@ -262,7 +265,7 @@ void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
   constexpr int NT = 64 * (TM / WM) * (TN / WN);
   // the window form for convs of >= 5 taps on the vectorised path (span within the staged rows);
   // at 3 taps the extra barrier per chunk outweighs the saved loads (profiles/ubench_vocoder_r02_win.txt)
-  if (vec && a.ntaps >= 5 && a.span <= kWinSpan && igemm_win_enabled()) {
+  if (vec && a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled()) {
     const size_t lds = (size_t)(TM + kWinSpan + 2 * TN) * (KC * 2 + 16);
     hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT, true>), grid, dim3(NT), lds, s, a);
     return;
@@ -274,14 +277,34 @@ void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
     hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, false, OutT>), grid, dim3(NT), lds, s, a);
 }
 
+// tile configs (TM, TN, WM, WN, KC) of the two vocoder-dominant shapes, overridable for A/B builds
+#ifndef ITTS_IG_WIDE
+#define ITTS_IG_WIDE 128, 128, 64, 32, 64
+#endif
+#ifndef ITTS_IG_C192
+#define ITTS_IG_C192 128, 64, 32, 32, 64
+#endif
+#ifndef ITTS_IG_C192W  // Cout = 192 in the window form (convs of >= 5 taps): 256 rows, 8 waves of 64 x 32
+#define ITTS_IG_C192W 256, 64, 64, 32, 64
+#endif
+#ifndef ITTS_IG_WIDEW
+#define ITTS_IG_WIDEW ITTS_IG_WIDE
+#endif
 template <typename OutT>
 void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
   const bool wide_n = a.Cout >= 128, wide_k = a.Cin >= 128;
   // wide layers: 8 waves per 128 x 128 tile (64 x 32 each) -- more waves per CU to hide the staging
   // latency than 4 waves of 64 x 64 (+25-30 % on the latent-pass GEMMs, profiles/ubench_igemm.py);
-  // Cout = 192 (stage 2): 128 x 64 tiles of 8 x (32 x 32) instead of a half-empty second 128-column tile
-  if (wide_n && wide_k && a.Cout % 128 == 0) launch_cfg<128, 128, 64, 32, 64, OutT>(a, vec, s);
-  else if (wide_n && wide_k && a.Cout % 64 == 0) launch_cfg<128, 64, 32, 32, 64, OutT>(a, vec, s);
+  // Cout = 192 (stage 2): 64-column tiles instead of a half-empty second 128-column tile; in the
+  // window form 256 x 64 tiles of 8 x (64 x 32) (conv k = 11: 1247 -> 912 us, profiles/igemm_ab_r02.txt)
+  const bool win = vec && a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled();
+  if (wide_n && wide_k && a.Cout % 128 == 0) {
+    if (win) launch_cfg<ITTS_IG_WIDEW, OutT>(a, vec, s);
+    else launch_cfg<ITTS_IG_WIDE, OutT>(a, vec, s);
+  } else if (wide_n && wide_k && a.Cout % 64 == 0) {
+    if (win) launch_cfg<ITTS_IG_C192W, OutT>(a, vec, s);
+    else launch_cfg<ITTS_IG_C192, OutT>(a, vec, s);
+  }
   else if (wide_n && wide_k) launch_cfg<128, 128, 64, 64, 64, OutT>(a, vec, s);
   else if (wide_n) launch_cfg<128, 128, 64, 64, 32, OutT>(a, vec, s);
   else if (wide_k) launch_cfg<128, 32, 32, 32, 64, OutT>(a, vec, s);
