@@ -16,7 +16,7 @@
 // through double-buffered LDS (row pitch padded by 16 B -> conflict-free ds_read_b128 fragments),
 // with a 3-deep register ring (K-step it+2's global loads in flight while step it computes).
 // Tiles are remapped XCD-aware (output-channel tiles of one row tile run together on one XCD).
-// WIN (convs of >= 5 taps, tap span <= 64 rows): K steps run channel chunk outer, tap inner, and the A
+// WIN (convs of >= 3 taps, tap span <= 64 rows): K steps run channel chunk outer, tap inner, and the A
 // operand of a chunk is ONE input window of TM + span rows staged once for all its taps (tap j reads
 // it at row offset off_j - min_off), instead of TM rows per tap: an 11-tap conv moves 178 input rows
 // per chunk through L2 -> LDS instead of 1408.
@@ -29,7 +29,7 @@ namespace {
 constexpr int kMaxTaps = 16;
 constexpr int kWinSpan = 64;  // WIN: max tap span (rows)
 #ifndef ITTS_IG_WIN_MINTAPS  // fewest taps that take the window form
-#define ITTS_IG_WIN_MINTAPS 5
+#define ITTS_IG_WIN_MINTAPS 3
 #endif
 
 struct IgArgs {
@@ -263,8 +263,9 @@ template <int TM, int TN, int WM, int WN, int KC, typename OutT>
 void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
   dim3 grid(((a.Tmax + TM - 1) / TM) * ((a.Cout + TN - 1) / TN) * a.B);
   constexpr int NT = 64 * (TM / WM) * (TN / WN);
-  // the window form for convs of >= 5 taps on the vectorised path (span within the staged rows);
-  // at 3 taps the extra barrier per chunk outweighs the saved loads (profiles/ubench_vocoder_r02_win.txt)
+  // the window form for convs of >= 3 taps on the vectorised path (span within the staged rows);
+  // with 128 x 128 / 128 x 64 tiles 3 taps were a wash (profiles/ubench_vocoder_r02_win.txt), with the
+  // 256 x 64 Cout = 192 tile the window form wins there too (572 -> 532 us, profiles/igemm_ab_r02.txt)
   if (vec && a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled()) {
     const size_t lds = (size_t)(TM + kWinSpan + 2 * TN) * (KC * 2 + 16);
     hipLaunchKernelGGL((igemm_kernel<TM, TN, WM, WN, KC, true, OutT, true>), grid, dim3(NT), lds, s, a);
@@ -284,7 +285,7 @@ void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
 #ifndef ITTS_IG_C192
 #define ITTS_IG_C192 128, 64, 32, 32, 64
 #endif
-#ifndef ITTS_IG_C192W  // Cout = 192 in the window form (convs of >= 5 taps): 256 rows, 8 waves of 64 x 32
+#ifndef ITTS_IG_C192W  // Cout = 192 in the window form: 256 rows, 8 waves of 64 x 32
 #define ITTS_IG_C192W 256, 64, 64, 32, 64
 #endif
 #ifndef ITTS_IG_WIDEW
