@@ -172,14 +172,18 @@ def test_activation_kernel_f16_bct(golden, i):
     assert rc != 0 and b"f16" in lib.itts_last_error()
 
 
-@pytest.mark.parametrize("cin,cout,k,d", [(768, 768, 3, 5), (96, 96, 11, 3), (24, 24, 7, 1), (1024, 1536, 7, 1),
-                                          (12, 6, 3, 1), (40, 200, 5, 2)])
-def test_igemm_conv_matches_torch(cin, cout, k, d):
+@pytest.mark.parametrize("cin,cout,k,d,T", [(768, 768, 3, 5, 150), (96, 96, 11, 3, 150), (24, 24, 7, 1, 150),
+                                            (1024, 1536, 7, 1, 150), (12, 6, 3, 1, 150), (40, 200, 5, 2, 150),
+                                            # Cout = 192: 256 x 64 window tiles (k >= 3), 128 x 64 at 1 tap;
+                                            # several row tiles, a ragged second row
+                                            (192, 192, 11, 5, 600), (192, 192, 3, 1, 600), (384, 192, 1, 1, 600),
+                                            (768, 768, 7, 3, 600)])
+def test_igemm_conv_matches_torch(cin, cout, k, d, T):
     from indextts.vocoder.bigvgan import _Conv, conv1d_taps
     _hip, lib = _lib()
-    torch.manual_seed(cin + cout)
-    B, T = 2, 150
-    lens = torch.tensor([150, 61], dtype=torch.int32)
+    torch.manual_seed(cin + cout + k)
+    B = 2
+    lens = torch.tensor([T, T // 2 + 1], dtype=torch.int32)
     x = torch.randn(B, T, cin).to(torch.bfloat16)
     w = torch.randn(cout, cin, k) / (cin * k) ** 0.5
     bias = torch.randn(cout) * 0.1
@@ -274,7 +278,10 @@ def test_vocoder_ragged_batch_equals_single():
 
 @pytest.mark.parametrize("C,k,d,use_act,nres,alpha", [(24, 7, 3, True, 1, 1.0), (48, 11, 5, True, 2, 1.0 / 3),
                                                      (96, 3, 1, False, 0, 1.0), (24, 3, 1, True, 0, 1.0),
-                                                     (96, 11, 5, True, 1, 1.0), (48, 7, 1, False, 2, 0.5)])
+                                                     (96, 11, 5, True, 1, 1.0), (48, 7, 1, False, 2, 0.5),
+                                                     # the product's conv-only forms (activation in its own kernel)
+                                                     (24, 11, 5, False, 1, 1.0), (48, 11, 5, False, 1, 1.0),
+                                                     (96, 7, 3, False, 2, 0.5)])
 def test_amp_conv_matches_torch(C, k, d, use_act, nres, alpha):
     """itts_amp_conv_fwd = alpha * (conv(act(x)) + bias + r1 + r2) on a ragged batch vs torch fp32 with
     the torch-path Activation1d (oracle) rounded to bf16 as the kernel stages it.
