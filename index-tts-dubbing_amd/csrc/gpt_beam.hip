@@ -216,12 +216,12 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
     return;
   }
   // ---- sampling with warpers: Temperature -> TopK (k' = max(top_k, 2), ties kept) -> TopP (min 2)
-  for (int i = 0; i < kPer; ++i) {
-    const int t = 4 * (threadIdx.x + kT * (i / 4)) + (i & 3);
-    if (t < p.V) sc[t] = v[i] * p.inv_temp;
-  }
-  __syncthreads();
   if (p.top_k > kMaxK || p.top_k <= 0) {
+    for (int i = 0; i < kPer; ++i) {
+      const int t = 4 * (threadIdx.x + kT * (i / 4)) + (i & 3);
+      if (t < p.V) sc[t] = v[i] * p.inv_temp;
+    }
+    __syncthreads();
     // any top_k, or top-p only: survivors = keys >= the warper threshold (select.h); Gumbel keys of
     // the survivors in place, then the row's C best keys by C rounds of block argmax
     const uint32_t T = itts_select::warper_threshold(sc, p.V, p.top_k, p.top_p, 2, hist, bc, rv);
@@ -255,20 +255,47 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
     }
     return;
   }
+  // 0 < top_k <= 64: the survivors leave in descending (score, lowest index first) order by repeated
+  // block argmax over the register-resident scores; the winner's owner clears it and rescans its own
+  // registers.  One barrier per round (the wave winners alternate between two LDS slots).  The LDS-
+  // staged form (one thread rescanning its 32-entry LDS slice per round, two barriers) took 128 us
+  // of a 96-row beam3 step (profiles/kernel_stats_r02f_beam3.txt).
   const int kk = p.top_k < 2 ? 2 : p.top_k;
-  float mine = -INFINITY;
-  int mine_i = 0x7fffffff;
-  for (int t = threadIdx.x; t < p.V; t += kT)
-    if (better(sc[t], t, mine, mine_i)) {
-      mine = sc[t];
-      mine_i = t;
-    }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) v[i] *= p.inv_temp;  // -inf stays -inf (inv_temp > 0)
+  auto tok = [](int i) { return 4 * ((int)threadIdx.x + kT * (i / 4)) + (i & 3); };
+  float mine, nxt;
+  int mine_i, nxt_i;
+  {
+    const itts_select::Top2 t2 = itts_select::top2_after(v, tok, INFINITY, -1);
+    mine = t2.b1;
+    mine_i = t2.i1;
+    nxt = t2.b2;
+    nxt_i = t2.i2;
+  }
+  bool has_nxt = ITTS_TOPK_CACHE2 != 0;
+  __shared__ uint32_t wk2[2][2][kT / 64];  // [slot][hi, lo][wave]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int nc = 0;
   float tau = -INFINITY;
   while (nc < kMaxK) {
-    float bv = mine;
-    int bidx = mine_i;
-    block_argmax<kT>(bv, bidx, rv, ri);
+    // the round's winner: one max over (score, token) keys -- DPP within the wave, the 4 wave maxima
+    // through LDS (two slots: a slot is rewritten two rounds later, after the next round's barrier)
+    const itts_select::Key64 wk = itts_select::wave_max_key64(itts_select::key64(mine, mine_i));
+    const int slot = nc & 1;
+    if (lane == 0) {
+      wk2[slot][0][wid] = wk.hi;
+      wk2[slot][1][wid] = wk.lo;
+    }
+    __syncthreads();
+    itts_select::Key64 bk{wk2[slot][0][0], wk2[slot][1][0]};
+#pragma unroll
+    for (int w = 1; w < kT / 64; ++w) {
+      const itts_select::Key64 o{wk2[slot][0][w], wk2[slot][1][w]};
+      if (itts_select::key64_gt(o, bk)) bk = o;
+    }
+    const float bv = itts_select::key64_score(bk);
+    const int bidx = (int)~bk.lo;
     if (bv == -INFINITY || !(bv == bv)) break;
     if (nc >= kk && bv < tau) break;  // HF keeps every score >= the k-th largest
     if (threadIdx.x == 0) {
@@ -277,15 +304,19 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
     }
     if (nc == kk - 1) tau = bv;
     ++nc;
-    if ((bidx % kT) == (int)threadIdx.x) {
-      sc[bidx] = -INFINITY;
-      mine = -INFINITY;
-      mine_i = 0x7fffffff;
-      for (int t = threadIdx.x; t < p.V; t += kT)
-        if (better(sc[t], t, mine, mine_i)) {
-          mine = sc[t];
-          mine_i = t;
-        }
+    if (mine_i == bidx) {  // the owner (tokens are unique): next candidate = its cached second
+      if (has_nxt) {
+        mine = nxt;
+        mine_i = nxt_i;
+        has_nxt = false;
+      } else {
+        const itts_select::Top2 t2 = itts_select::top2_after(v, tok, bv, bidx);
+        mine = t2.b1;
+        mine_i = t2.i1;
+        nxt = t2.b2;
+        nxt_i = t2.i2;
+        has_nxt = ITTS_TOPK_CACHE2 != 0;
+      }
     }
   }
   if (threadIdx.x == 0) {
@@ -648,7 +679,8 @@ extern "C" int itts_beam_candidates(const float* logits, int64_t ldl, int V, con
   ITTS_REQUIRE(!do_sample || top_k >= 0, fn, "top_k must be >= 0");
   BeamArgs a{logits, ldl, V, const_cast<uint8_t*>(seen), beam_score, tstate, col_delta, min_new, stop, penalty,
              do_sample, do_sample ? 1.f / temperature : 1.f, top_k, top_p, num_beams, cand_key, cand_score, cand_tok};
-  const size_t lds = (do_sample && (top_k > 0 || top_p < 1.f)) ? (size_t)V * sizeof(float) : 0;
+  // the LDS-staged row is only for the general warper path (top_k > 64, or top-p alone)
+  const size_t lds = (do_sample && (top_k > kMaxK || (top_k <= 0 && top_p < 1.f))) ? (size_t)V * sizeof(float) : 0;
   ITTS_REQUIRE(lds <= 64 * 1024 - 2048, fn, "vocabulary too large for the LDS score buffer");
   hipLaunchKernelGGL(beam_cand_kernel, dim3(R), dim3(kT), lds, itts::as_stream(stream), a);
   return itts::check_launch(fn);

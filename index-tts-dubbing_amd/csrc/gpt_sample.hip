@@ -221,6 +221,47 @@ __global__ __launch_bounds__(kT) void sample_embed_kernel(SampleArgs p) {
 // of its own strided slice, only the winner rescans); top-p + the multinomial draw run on the
 // candidates.  top_k > 64 or top-p alone: warper thresholds (select.h) + a Gumbel-max draw among the
 // survivors.  top_k == 0 and top_p == 1: Gumbel-max draw over the whole vocabulary.
+constexpr int kRegS = 33;  // register-resident row: ceil(8194 / 256) scores per thread
+
+// thread 0: TopP over the nc top-k candidates (descending), then the multinomial draw -> ri[0]
+__device__ __forceinline__ void topk_top_p_pick(const SampleArgs& p, const float* cv, const int* ci, int nc,
+                                                uint64_t key, float* rv, int* ri) {
+  int pick = nc > 0 ? ci[0] : p.stop;
+  if (nc > 1) {
+    // softmax over the candidates (all other scores are -inf after top-k)
+    float e[kMaxK];
+    float z = 0.f;
+    for (int i = 0; i < nc; ++i) {
+      e[i] = __expf(cv[i] - cv[0]);
+      z += e[i];
+    }
+    // TopP: ascending cumulative probability; drop while cum <= 1 - top_p; keep the largest
+    int keep = nc;
+    if (p.top_p < 1.f) {
+      float cum = 0.f;
+      for (int i = nc - 1; i > 0; --i) {
+        cum += e[i] / z;
+        if (cum <= 1.f - p.top_p) keep = i;
+        else break;
+      }
+    }
+    float zk = 0.f;
+    for (int i = 0; i < keep; ++i) zk += e[i];
+    const float u = uniform01(key) * zk;
+    float acc = 0.f;
+    pick = ci[keep - 1];
+    for (int i = 0; i < keep; ++i) {
+      acc += e[i];
+      if (u < acc) {
+        pick = ci[i];
+        break;
+      }
+    }
+  }
+  rv[0] = 0.f;
+  ri[0] = pick;
+}
+
 template <typename TH>
 __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
   extern __shared__ float sc[];  // [V]
@@ -265,6 +306,77 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
       }
     }
     block_argmax(best, bi, rv, ri);
+  } else if (p.V <= kT * kRegS) {
+    // 0 < top_k <= 64, row in registers (element j*kT + tid): repeated block argmax with one barrier
+    // per round (wave winners alternate between two LDS slots); the winner's owner clears it and
+    // rescans its registers.  Same candidates, same order as the LDS-staged form below (the IndexTTS
+    // vocabulary always takes this path).
+    float s[kRegS];
+#pragma unroll
+    for (int j = 0; j < kRegS; ++j) {
+      const int v = threadIdx.x + kT * j;
+      s[j] = v < p.V ? processed_score(p, lr, sr, v, col) * p.inv_temp : -INFINITY;
+    }
+    auto tok = [](int j) { return (int)threadIdx.x + kT * j; };
+    __shared__ uint32_t wk2[2][2][kT / 64];  // [slot][hi, lo][wave]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    float mine, nxt;
+    int mine_i, nxt_i;
+    {
+      const itts_select::Top2 t2 = itts_select::top2_after(s, tok, INFINITY, -1);
+      mine = t2.b1;
+      mine_i = t2.i1;
+      nxt = t2.b2;
+      nxt_i = t2.i2;
+    }
+    bool has_nxt = ITTS_TOPK_CACHE2 != 0;
+    int nc = 0;
+    float tau = -INFINITY;
+    while (nc < kMaxK) {
+      // the round's winner: one max over (score, token) keys -- DPP within the wave, the 4 wave maxima
+      // through LDS (two slots: a slot is rewritten two rounds later, after the next round's barrier)
+      const itts_select::Key64 wk = itts_select::wave_max_key64(itts_select::key64(mine, mine_i));
+      const int slot = nc & 1;
+      if (lane == 0) {
+        wk2[slot][0][wid] = wk.hi;
+        wk2[slot][1][wid] = wk.lo;
+      }
+      __syncthreads();
+      itts_select::Key64 bk{wk2[slot][0][0], wk2[slot][1][0]};
+#pragma unroll
+      for (int w = 1; w < kT / 64; ++w) {
+        const itts_select::Key64 o{wk2[slot][0][w], wk2[slot][1][w]};
+        if (itts_select::key64_gt(o, bk)) bk = o;
+      }
+      const float bv = itts_select::key64_score(bk);
+      const int bidx = (int)~bk.lo;
+      if (bv == -INFINITY || !(bv == bv)) break;
+      if (nc >= p.top_k && bv < tau) break;  // HF keeps every score >= the k-th largest
+      if (threadIdx.x == 0) {
+        cv[nc] = bv;
+        ci[nc] = bidx;
+      }
+      if (nc == p.top_k - 1) tau = bv;
+      ++nc;
+      if (mine_i == bidx) {  // the owner (tokens are unique): next candidate = its cached second
+        if (has_nxt) {
+          mine = nxt;
+          mine_i = nxt_i;
+          has_nxt = false;
+        } else {
+          const itts_select::Top2 t2 = itts_select::top2_after(s, tok, bv, bidx);
+          mine = t2.b1;
+          mine_i = t2.i1;
+          nxt = t2.b2;
+          nxt_i = t2.i2;
+          has_nxt = ITTS_TOPK_CACHE2 != 0;
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) topk_top_p_pick(p, cv, ci, nc, key, rv, ri);
+    __syncthreads();
+    bi = ri[0];
   } else {
     for (int v = threadIdx.x; v < p.V; v += kT) {
       const float s = processed_score(p, lr, sr, v, col) * p.inv_temp;
@@ -302,42 +414,7 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
       }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int pick = nc > 0 ? ci[0] : p.stop;
-      if (nc > 1) {
-        // softmax over the candidates (all other scores are -inf after top-k)
-        float e[kMaxK];
-        float z = 0.f;
-        for (int i = 0; i < nc; ++i) {
-          e[i] = __expf(cv[i] - cv[0]);
-          z += e[i];
-        }
-        // TopP: ascending cumulative probability; drop while cum <= 1 - top_p; keep the largest
-        int keep = nc;
-        if (p.top_p < 1.f) {
-          float cum = 0.f;
-          for (int i = nc - 1; i > 0; --i) {
-            cum += e[i] / z;
-            if (cum <= 1.f - p.top_p) keep = i;
-            else break;
-          }
-        }
-        float zk = 0.f;
-        for (int i = 0; i < keep; ++i) zk += e[i];
-        const float u = uniform01(key) * zk;
-        float acc = 0.f;
-        pick = ci[keep - 1];
-        for (int i = 0; i < keep; ++i) {
-          acc += e[i];
-          if (u < acc) {
-            pick = ci[i];
-            break;
-          }
-        }
-      }
-      rv[0] = 0.f;
-      ri[0] = pick;
-    }
+    if (threadIdx.x == 0) topk_top_p_pick(p, cv, ci, nc, key, rv, ri);
     __syncthreads();
     bi = ri[0];
   }

@@ -42,6 +42,85 @@ __device__ __forceinline__ float block_max(float v, float* red4) {
   return fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
 }
 
+// Top-k extraction loops: 1 = a winner's owner takes its cached second best as its next candidate
+// (rescans only when it wins twice), 0 = the owner rescans its registers after every win.
+#ifndef ITTS_TOPK_CACHE2
+#define ITTS_TOPK_CACHE2 1
+#endif
+
+// (score desc, index asc) order of the top-k extraction loops
+__device__ __forceinline__ bool before(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
+
+// Best two of a thread's register-resident scores s[i] (token idx(i)) among those that come after
+// (lv, li) in the extraction order (every score before it has already left).  The top-k loops keep
+// the second as the owner's next candidate, so a winner's owner rescans only when it wins twice.
+struct Top2 {
+  float b1;
+  int i1;
+  float b2;
+  int i2;
+};
+template <int N, typename IdxF>
+__device__ __forceinline__ Top2 top2_after(const float (&s)[N], IdxF idx, float lv, int li) {
+  Top2 r{-INFINITY, 0x7fffffff, -INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int t = idx(i);
+    const float x = s[i];
+    const bool ok = before(lv, li, x, t);
+    const bool f1 = ok && before(x, t, r.b1, r.i1);
+    const bool f2 = ok && !f1 && before(x, t, r.b2, r.i2);
+    // branch-free: every lane runs the same selects (the owner is a single lane)
+    r.b2 = f1 ? r.b1 : (f2 ? x : r.b2);
+    r.i2 = f1 ? r.i1 : (f2 ? t : r.i2);
+    r.b1 = f1 ? x : r.b1;
+    r.i1 = f1 ? t : r.i1;
+  }
+  return r;
+}
+
+// (score, token) as one 64-bit key whose unsigned order is the extraction order: hi = okey(score)
+// (zeros canonicalised: -0 and +0 compare equal as floats, the token then decides), lo = ~token.
+// NaN maps to 0 (below every score, decodes to NaN, which ends a top-k loop as before()'s never-winning
+// NaN does).
+struct Key64 {
+  uint32_t hi, lo;
+};
+__device__ __forceinline__ Key64 key64(float v, int t) {
+  if (!(v == v)) return {0u, 0u};
+  return {okey(v + 0.0f), ~(uint32_t)t};
+}
+__device__ __forceinline__ float key64_score(const Key64& k) {
+  return __uint_as_float((k.hi & 0x80000000u) ? (k.hi & 0x7fffffffu) : ~k.hi);
+}
+__device__ __forceinline__ bool key64_gt(const Key64& a, const Key64& b) {
+  return (a.hi > b.hi) | ((a.hi == b.hi) & (a.lo > b.lo));
+}
+template <int CTRL>
+__device__ __forceinline__ void key64_max_dpp(Key64& k) {
+  const Key64 o{(uint32_t)__builtin_amdgcn_mov_dpp((int)k.hi, CTRL, 0xF, 0xF, false),
+                (uint32_t)__builtin_amdgcn_mov_dpp((int)k.lo, CTRL, 0xF, 0xF, false)};
+  const bool t = key64_gt(o, k);
+  k.hi = t ? o.hi : k.hi;
+  k.lo = t ? o.lo : k.lo;
+}
+// wave-wide max key, uniform in every lane: DPP within each 16-lane row (quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror -- VALU operands, no LDS round trip), then the 4 row maxima by readlane
+__device__ __forceinline__ Key64 wave_max_key64(Key64 k) {
+  key64_max_dpp<0xB1>(k);   // quad_perm [1,0,3,2]
+  key64_max_dpp<0x4E>(k);   // quad_perm [2,3,0,1]
+  key64_max_dpp<0x141>(k);  // row_half_mirror
+  key64_max_dpp<0x140>(k);  // row_mirror
+  Key64 w{(uint32_t)__builtin_amdgcn_readlane((int)k.hi, 0), (uint32_t)__builtin_amdgcn_readlane((int)k.lo, 0)};
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {
+    const Key64 o{(uint32_t)__builtin_amdgcn_readlane((int)k.hi, 16 * r),
+                  (uint32_t)__builtin_amdgcn_readlane((int)k.lo, 16 * r)};
+    if (key64_gt(o, w)) w = o;
+  }
+  return w;
+}
+
 // key of the k-th largest score (1 <= k <= V); hist: 256 ints of LDS, bc: 2 ints of LDS
 __device__ inline uint32_t kth_largest_key(const float* sc, int V, int k, int* hist, int* bc) {
   uint32_t prefix = 0, mask = 0;

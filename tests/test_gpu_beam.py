@@ -113,3 +113,87 @@ def test_beam_sample_distribution_matches_oracle(beam_golden, top_k, top_p):
     again = eng.generate(conds.cuda(), text.cuda().expand(N, -1).contiguous(), 3, num_beams=3, do_sample=True,
                          top_k=top_k, top_p=top_p, seed=123).cpu().numpy()
     np.testing.assert_array_equal(again, got)
+
+
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def _gumbel(key):
+    u = (float(_mix64(key & _M64) >> 40) + 0.5) * 5.9604645e-8
+    return -np.log(-np.log(u))
+
+
+@pytest.mark.parametrize("top_k,top_p", [(30, 0.8), (2, 1.0), (64, 0.95), (5, 0.3)])
+def test_beam_candidates_top_k_path_vs_restatement(top_k, top_p):
+    """itts_beam_candidates, beam sample with 0 < top_k <= 64 (the reference default top_k 30,
+    top_p 0.8 among them), vs a numpy restatement of gpt_beam.hip's contract: log_softmax ->
+    repetition penalty -> / T -> TopK (ties at the k-th score kept, <= 64) -> TopP (min 2) ->
+    + beam score -> the row's 2K best Gumbel keys (same counter-based noise).  Tokens exact, scores
+    and keys to f32 rounding.  Ties are planted at the k-th score."""
+    from indextts import _hip
+    lib = _hip.load()
+    K, B, V = 3, 4, 8194
+    R, C = K * B, 2 * K
+    ldl = (V + 3) // 4 * 4
+    rng = np.random.default_rng(7 + top_k)
+    logits = (rng.standard_normal((R, ldl)) * 3).astype(np.float32)
+    seen = (rng.random((R, ldl)) < 0.02).astype(np.uint8)
+    for r in range(R):  # ties around rank top_k (distinct tokens, equal logits, equal seen flags)
+        order = np.argsort(-logits[r, :V], kind="stable")
+        logits[r, order[max(top_k - 2, 0): top_k + 2]] = logits[r, order[top_k - 1]]
+        seen[r, order[max(top_k - 2, 0): top_k + 2]] = 0
+    bscore = (rng.standard_normal(R) * 2).astype(np.float32)
+    col, row0, seed = 17, 5, 0x1234_5678_9ABC
+    tstate = np.array([col, row0, seed & 0xFFFFFFFF, seed >> 32], dtype=np.int32)
+    temp, pen, stop, min_new = 0.9, 1.3, 8193, 0
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    lg, sn, bs, ts = d(logits), d(seen), d(bscore), d(tstate)
+    ck = torch.empty(R, C, device="cuda")
+    cs = torch.empty(R, C, device="cuda")
+    ct = torch.empty(R, C, dtype=torch.int32, device="cuda")
+    _hip.check(lib.itts_beam_candidates(lg.data_ptr(), ldl, V, sn.data_ptr(), bs.data_ptr(), ts.data_ptr(), 0, min_new,
+                                        stop, pen, 1, temp, top_k, top_p, K, ck.data_ptr(), cs.data_ptr(),
+                                        ct.data_ptr(), R, _hip.stream_ptr()), "itts_beam_candidates")
+    torch.cuda.synchronize()
+    ck, cs, ct = ck.cpu().numpy(), cs.cpu().numpy(), ct.cpu().numpy()
+    for r in range(R):
+        x = logits[r, :V].astype(np.float64)
+        x = x - (x.max() + np.log(np.exp(x - x.max()).sum()))
+        x = np.where(seen[r, :V] > 0, np.where(x < 0, x * pen, x / pen), x)
+        s = (x / temp).astype(np.float32)
+        order = np.lexsort((np.arange(V), -s))
+        kk = max(top_k, 2)
+        tk, tau = [], -np.inf
+        for nc, t in enumerate(order[:64]):
+            if nc >= kk and s[t] < tau:
+                break
+            tk.append(int(t))
+            if nc == kk - 1:
+                tau = s[t]
+        keep = len(tk)
+        if top_p < 1.0 and keep > 2:
+            e = np.exp(s[tk].astype(np.float64) - s[tk[0]])
+            cum = 0.0
+            for i in range(len(tk) - 1, 1, -1):
+                cum += e[i] / e.sum()
+                if cum <= 1.0 - top_p:
+                    keep = i
+                else:
+                    break
+        tk = tk[:keep]
+        rkey = _mix64(seed ^ _mix64((((r + row0) & 0xFFFFFFFF) << 32) | col))
+        score = np.array([s[t] + bscore[r] for t in tk])
+        key = np.array([score[i] + _gumbel(rkey + t + 1) for i, t in enumerate(tk)])
+        best = np.lexsort((np.array(tk), -key))[:C]
+        n = len(best)
+        assert ct[r].tolist() == [tk[i] for i in best] + [stop] * (C - n), (r, ct[r], [tk[i] for i in best])
+        np.testing.assert_allclose(cs[r, :n], score[best], rtol=0, atol=2e-4)
+        np.testing.assert_allclose(ck[r, :n], key[best], rtol=0, atol=2e-3)
+        assert np.all(np.isneginf(ck[r, n:])) and np.all(np.isneginf(cs[r, n:]))
