@@ -240,7 +240,7 @@ int itts_sample_topk_embed(const float* logits, int64_t ldl, int V, uint8_t* see
                            float temperature, int top_k, float top_p, const float* emb, const float* pos_emb,
                            int pos_delta, int D, const float* ln_g, const float* ln_b, float* x, void* h,
                            int h_dtype, int B, const int32_t* forced, void* stream);
-/* Beam search / beam sample step, part 1 (rows R = utterances x num_beams, 2 <= num_beams <= 8):
+/* Beam search / beam sample step, part 1 (rows R = utterances x num_beams, 2 <= num_beams <= 16):
  * per row log_softmax -> repetition penalty on the log-probs (Q4) -> min_new_tokens -> [do_sample:
  * Temperature -> TopK -> TopP, min_keep 2] -> + running beam score; writes the row's 2*num_beams best
  * (key, score, token) candidates (key = score, or score + Gumbel noise when sampling: a without-

@@ -25,7 +25,7 @@
 
 namespace {
 constexpr int kT = 256;
-constexpr int kMaxBeams = 8;
+constexpr int kMaxBeams = 16;  // num_beams <= 16 (candidate tables in LDS, 8 per lane in the merge)
 constexpr int kMaxC = 2 * kMaxBeams;  // candidates per row / per utterance
 constexpr int kMaxK = 64;             // top-k cap of the sampling warper
 
@@ -123,7 +123,13 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
   const float bs = p.beam_score[r];
   // registers: element v = 4 * (threadIdx.x + kT * i) + e
   float v[kPer];
+  uint32_t s4r[kPer / 4];  // seen flags, requested with the logits (one memory round trip, not two)
   float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < kPer / 4; ++i) {
+    const int v4 = threadIdx.x + kT * i;
+    s4r[i] = 4 * v4 < p.V ? reinterpret_cast<const uint32_t*>(sr)[v4] : 0u;
+  }
 #pragma unroll
   for (int i = 0; i < kPer / 4; ++i) {
     const int v4 = threadIdx.x + kT * i;
@@ -146,8 +152,7 @@ __global__ __launch_bounds__(kT) void beam_cand_kernel(BeamArgs p) {
 #pragma unroll
   for (int i = 0; i < kPer / 4; ++i) {
     const int v4 = threadIdx.x + kT * i;
-    uint32_t s4 = 0;
-    if (4 * v4 < p.V) s4 = reinterpret_cast<const uint32_t*>(sr)[v4];
+    const uint32_t s4 = s4r[i];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int t = 4 * v4 + e;
@@ -442,19 +447,30 @@ __global__ __launch_bounds__(kT) void beam_select_kernel(SelArgs p) {
       s_par[i] = i / C;
     }
     __syncthreads();
-    // the utterance's C best keys (one wave; ties -> lower flat index beam * V + token)
+    // the utterance's C best keys (one wave, up to 8 candidates per lane; ties -> lower flat index
+    // beam * V + token)
     if (threadIdx.x < 64) {
       const int lane = threadIdx.x;
-      float k0 = lane < K * C ? s_key[lane] : -INFINITY;
-      float k1 = lane + 64 < K * C ? s_key[lane + 64] : -INFINITY;
-      const int f0 = lane < K * C ? s_par[lane] * p.V + s_tok[lane] : 0x7fffffff;
-      const int f1 = lane + 64 < K * C ? s_par[lane + 64] * p.V + s_tok[lane + 64] : 0x7fffffff;
+      constexpr int NPL = kMaxBeams * kMaxC / 64;
+      float kk[NPL];
+      int ff[NPL];
+#pragma unroll
+      for (int j = 0; j < NPL; ++j) {
+        const int i = lane + 64 * j;
+        kk[j] = i < K * C ? s_key[i] : -INFINITY;
+        ff[j] = i < K * C ? s_par[i] * p.V + s_tok[i] : 0x7fffffff;
+      }
       int n = 0;
       for (int c = 0; c < C; ++c) {
-        const bool use1 = k1 > k0 || (k1 == k0 && f1 < f0);
-        float bk = use1 ? k1 : k0;
-        int bf = use1 ? f1 : f0;
-        int bs = use1 ? lane + 64 : lane;
+        float bk = kk[0];
+        int bf = ff[0], bs = lane;
+#pragma unroll
+        for (int j = 1; j < NPL; ++j) {
+          const bool u = kk[j] > bk || (kk[j] == bk && ff[j] < bf);
+          bk = u ? kk[j] : bk;
+          bf = u ? ff[j] : bf;
+          bs = u ? lane + 64 * j : bs;
+        }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
           const float ok = __shfl_xor(bk, o, 64);
@@ -473,8 +489,9 @@ __global__ __launch_bounds__(kT) void beam_select_kernel(SelArgs p) {
           top_tok[c] = s_tok[bs];
           top_par[c] = s_par[bs];
         }
-        if (bs == lane) k0 = -INFINITY;
-        if (bs == lane + 64) k1 = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < NPL; ++j)
+          if (bs == lane + 64 * j) kk[j] = -INFINITY;
         ++n;
       }
       if (lane == 0) ntop = n;
@@ -668,7 +685,7 @@ extern "C" int itts_beam_candidates(const float* logits, int64_t ldl, int V, con
                                     int do_sample, float temperature, int top_k, float top_p, int num_beams,
                                     float* cand_key, float* cand_score, int32_t* cand_tok, int R, void* stream) {
   const char* fn = "itts_beam_candidates";
-  ITTS_REQUIRE(R >= 0 && V > 0 && num_beams >= 2 && num_beams <= kMaxBeams, fn, "bad sizes (2 <= num_beams <= 8)");
+  ITTS_REQUIRE(R >= 0 && V > 0 && num_beams >= 2 && num_beams <= kMaxBeams, fn, "bad sizes (2 <= num_beams <= 16)");
   if (R == 0) return 0;
   ITTS_REQUIRE(R % num_beams == 0, fn, "rows must be utterances x num_beams");
   ITTS_REQUIRE(logits && seen && beam_score && tstate && cand_key && cand_score && cand_tok, fn, "null pointer");
@@ -705,11 +722,21 @@ extern "C" int itts_beam_select(const float* cand_key, const float* cand_score, 
   ITTS_REQUIRE(n_base >= 0 && num_beams * n_base <= kT, fn, "too many base ids");
   ITTS_REQUIRE(max_col >= 1 && max_col <= ldc && kv_base + max_col <= ld_rows, fn, "bad step capacity");
   const size_t lds_bytes = (size_t)2 * num_beams * max_col * sizeof(int32_t);
-  ITTS_REQUIRE(lds_bytes <= 48 * 1024, fn, "num_beams x max_new_tokens too large for the reorder buffer");
+  ITTS_REQUIRE(lds_bytes <= 144 * 1024, fn, "num_beams x max_new_tokens too large for the reorder buffer");
   SelArgs a{cand_key, cand_score, cand_tok, num_beams, V, stop, do_sample, length_penalty, tstate, col_delta, done,
             beam_score, codes, ldc, seen, lds, base_ids, n_base, kv_rows, ld_rows, kv_base, hyp_score, hyp_len,
             hyp_codes, hyp_n, hyp_order, hyp_worst, emb, pos_emb, pos_delta, D, ln_g, ln_b, x, h};
   hipStream_t s = itts::as_stream(stream);
+  if (lds_bytes > 64 * 1024) {  // beyond the default dynamic LDS cap (160 KiB per workgroup on gfx950)
+    static const bool once = [] {
+      const int cap = 144 * 1024;
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(beam_select_kernel<uint16_t>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, cap) == hipSuccess &&
+             hipFuncSetAttribute(reinterpret_cast<const void*>(beam_select_kernel<float>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, cap) == hipSuccess;
+    }();
+    ITTS_REQUIRE(once, fn, "could not raise the dynamic LDS limit for the reorder buffer");
+  }
   if (h_dtype == ITTS_BF16)
     hipLaunchKernelGGL(beam_select_kernel<uint16_t>, dim3(B), dim3(kT), lds_bytes, s, a);
   else

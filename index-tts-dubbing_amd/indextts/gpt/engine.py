@@ -807,7 +807,7 @@ class HipGPT:
         once per utterance (cache row b*K) and shared through the KV lineage table.
         -> codes [B, n] int64 (best hypothesis, then the stop token, padded with it)."""
         K = int(num_beams)
-        assert 2 <= K <= 8, "num_beams must be in [2, 8]"
+        assert 2 <= K <= 16, "num_beams must be in [2, 16]"
         emb, pad, s = self.prepare_inputs(conds, text_ids)
         B = emb.shape[0]
         R = B * K

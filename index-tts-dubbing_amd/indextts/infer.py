@@ -226,8 +226,8 @@ class IndexTTS:
         if kw:
             warnings.warn(f"ignored generation kwargs: {sorted(kw)}", RuntimeWarning)
         num_beams = int(num_beams or 1)
-        if num_beams > 8:
-            raise ValueError("HIP beam search supports num_beams <= 8")
+        if num_beams > 16:
+            raise ValueError("HIP beam search supports num_beams <= 16")
         smp = {}
         if num_beams > 1:
             smp = dict(num_beams=num_beams, length_penalty=float(length_penalty or 0.0))

@@ -197,3 +197,22 @@ def test_beam_candidates_top_k_path_vs_restatement(top_k, top_p):
         np.testing.assert_allclose(cs[r, :n], score[best], rtol=0, atol=2e-4)
         np.testing.assert_allclose(ck[r, :n], key[best], rtol=0, atol=2e-3)
         assert np.all(np.isneginf(ck[r, n:])) and np.all(np.isneginf(cs[r, n:]))
+
+
+@pytest.mark.parametrize("K", [5, 12, 16])
+def test_f32_wide_beam_search_matches_oracle(beam_golden, K):
+    """num_beams up to 16 (candidate tables of 16 x 32 in LDS, 8 per lane in the per-utterance merge):
+    f32 beam search ids equal the oracle's HF 4.36 beam_search restatement (pinned to the reference's
+    own num_beams = 2, 3 goldens, tests/test_oracle_beam.py) on the tiny config, single and padded
+    batch, with the stop logit raised so hypotheses close mid-run."""
+    from oracle.gpt_oracle import GPTOracle
+    bg = beam_golden
+    sd = _sd("tiny", 5.0, bg)
+    eng = _engine("tiny", "f32", 5.0, bg)
+    o = GPTOracle({k: v.clone() for k, v in sd.items()}, _cfg("tiny").gpt)
+    n = int(bg["tiny_steps"])
+    conds = torch.from_numpy(bg["tiny_conds"])
+    for text in (torch.from_numpy(bg["tiny_text"]), torch.from_numpy(bg["tiny_batch_text"])):
+        want = o.generate_beam(conds, text, n, num_beams=K).numpy()
+        got = eng.generate(conds.cuda(), text.cuda(), n, num_beams=K, check_every=1).cpu().numpy()
+        np.testing.assert_array_equal(got, want)

@@ -143,8 +143,9 @@ def test_decoding_kwargs():
     b = IndexTTS._decoding(dict(do_sample=False, num_beams=2, length_penalty=1.0))
     assert b == dict(max_mel_tokens=600, repetition_penalty=10.0, min_new_tokens=0, num_beams=2,
                      length_penalty=1.0)
+    assert IndexTTS._decoding(dict(num_beams=16))["num_beams"] == 16
     with pytest.raises(ValueError):
-        IndexTTS._decoding(dict(num_beams=9))
+        IndexTTS._decoding(dict(num_beams=17))
     g = IndexTTS._decoding(dict(do_sample=False, num_beams=1, max_mel_tokens=64))
     assert g == dict(max_mel_tokens=64, repetition_penalty=10.0, min_new_tokens=0)
     # top-p alone and top_k > 64 are supported (exact warper thresholds, csrc/select.h)
