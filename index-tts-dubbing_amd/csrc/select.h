@@ -16,6 +16,7 @@
 namespace itts_select {
 
 constexpr int kT = 256;
+constexpr int kRegRow = 36;  // register-resident row in the top-p descent: V <= 256 x 36 (IndexTTS: 8194)
 
 // order-preserving float -> uint32 (larger float, larger key; -inf maps below every finite score)
 __device__ __forceinline__ uint32_t okey(float f) {
@@ -121,7 +122,8 @@ __device__ __forceinline__ Key64 wave_max_key64(Key64 k) {
   return w;
 }
 
-// key of the k-th largest score (1 <= k <= V); hist: 256 ints of LDS, bc: 2 ints of LDS
+// key of the k-th largest score (1 <= k <= V); hist: 256 ints of LDS, bc: 2 ints of LDS (kT == 256:
+// one thread per histogram bin)
 __device__ inline uint32_t kth_largest_key(const float* sc, int V, int k, int* hist, int* bc) {
   uint32_t prefix = 0, mask = 0;
   for (int shift = 24; shift >= 0; shift -= 8) {
@@ -132,14 +134,26 @@ __device__ inline uint32_t kth_largest_key(const float* sc, int V, int k, int* h
       if ((kv & mask) == prefix) atomicAdd(&hist[(kv >> shift) & 255u], 1);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int cum = 0, d = 255;
-      for (; d > 0; --d) {
-        if (cum + hist[d] >= k) break;
-        cum += hist[d];
+    // the digit: the largest d with count(bins > d) < k <= count(bins >= d) (d = 0 if none), by a
+    // suffix scan over the 256 bins -- thread i owns bin 255 - i (wave scan, then the waves in order)
+    {
+      __shared__ int wtot[kT / 64];
+      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, d = 255 - (int)threadIdx.x;
+      const int c = hist[d];
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int up = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += up;
       }
-      bc[0] = d;
-      bc[1] = k - cum;
+      if (lane == 63) wtot[w] = incl;
+      __syncthreads();
+      for (int ww = 0; ww < w; ++ww) incl += wtot[ww];
+      const int excl = incl - c;
+      if (excl < k && (incl >= k || d == 0)) {
+        bc[0] = d;
+        bc[1] = k - excl;
+      }
     }
     __syncthreads();
     prefix |= (uint32_t)bc[0] << shift;
@@ -178,14 +192,34 @@ __device__ inline uint32_t warper_threshold(const float* sc, int V, int top_k, f
   // mass(T) = sum over survivors with key > T; non-increasing in T.  cur = the largest T with
   // mass(T) >= target (mass(0) = z >= target), built bit by bit; T* = cur + 1.
   uint32_t cur = 0;
-  for (int bit = 31; bit >= 0; --bit) {
-    const uint32_t cand = cur | (1u << bit);
-    float m = 0.f;
-    for (int v = threadIdx.x; v < V; v += kT) {
-      const uint32_t kv = okey(sc[v]);
-      if (kv >= tk && kv > cand) m += __expf(sc[v] - mx);
+  if (V <= kT * kRegRow) {
+    // the row's keys and exps held in registers once (same terms, same order as below; excluded
+    // entries add +0, which leaves a sum bitwise unchanged): 32 passes of compares and adds
+    uint32_t kr[kRegRow];
+    float er[kRegRow];
+#pragma unroll
+    for (int j = 0; j < kRegRow; ++j) {
+      const int v = threadIdx.x + kT * j;
+      kr[j] = v < V ? okey(sc[v]) : 0u;
+      er[j] = (v < V && kr[j] >= tk) ? __expf(sc[v] - mx) : 0.f;
     }
-    if (block_sum_fixed(m, red4) >= target) cur = cand;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = cur | (1u << bit);
+      float m = 0.f;
+#pragma unroll
+      for (int j = 0; j < kRegRow; ++j) m += kr[j] > cand ? er[j] : 0.f;
+      if (block_sum_fixed(m, red4) >= target) cur = cand;
+    }
+  } else {
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = cur | (1u << bit);
+      float m = 0.f;
+      for (int v = threadIdx.x; v < V; v += kT) {
+        const uint32_t kv = okey(sc[v]);
+        if (kv >= tk && kv > cand) m += __expf(sc[v] - mx);
+      }
+      if (block_sum_fixed(m, red4) >= target) cur = cand;
+    }
   }
   uint32_t tp = cur + 1u;
   if (min_keep > 1) {  // the min_keep best always survive

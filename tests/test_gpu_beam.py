@@ -130,7 +130,8 @@ def _gumbel(key):
     return -np.log(-np.log(u))
 
 
-@pytest.mark.parametrize("top_k,top_p", [(30, 0.8), (2, 1.0), (64, 0.95), (5, 0.3)])
+@pytest.mark.parametrize("top_k,top_p", [(30, 0.8), (2, 1.0), (64, 0.95), (5, 0.3), (100, 1.0), (0, 0.8),
+                                         (200, 0.9)])
 def test_beam_candidates_top_k_path_vs_restatement(top_k, top_p):
     """itts_beam_candidates, beam sample with 0 < top_k <= 64 (the reference default top_k 30,
     top_p 0.8 among them), vs a numpy restatement of gpt_beam.hip's contract: log_softmax ->
@@ -169,25 +170,39 @@ def test_beam_candidates_top_k_path_vs_restatement(top_k, top_p):
         x = np.where(seen[r, :V] > 0, np.where(x < 0, x * pen, x / pen), x)
         s = (x / temp).astype(np.float32)
         order = np.lexsort((np.arange(V), -s))
-        kk = max(top_k, 2)
-        tk, tau = [], -np.inf
-        for nc, t in enumerate(order[:64]):
-            if nc >= kk and s[t] < tau:
-                break
-            tk.append(int(t))
-            if nc == kk - 1:
-                tau = s[t]
-        keep = len(tk)
-        if top_p < 1.0 and keep > 2:
-            e = np.exp(s[tk].astype(np.float64) - s[tk[0]])
-            cum = 0.0
-            for i in range(len(tk) - 1, 1, -1):
-                cum += e[i] / e.sum()
-                if cum <= 1.0 - top_p:
-                    keep = i
-                else:
+        if 0 < top_k <= 64:  # register path: descending extraction, ties at the k-th kept (<= 64)
+            kk = max(top_k, 2)
+            tk, tau = [], -np.inf
+            for nc, t in enumerate(order[:64]):
+                if nc >= kk and s[t] < tau:
                     break
-        tk = tk[:keep]
+                tk.append(int(t))
+                if nc == kk - 1:
+                    tau = s[t]
+            keep = len(tk)
+            if top_p < 1.0 and keep > 2:
+                e = np.exp(s[tk].astype(np.float64) - s[tk[0]])
+                cum = 0.0
+                for i in range(len(tk) - 1, 1, -1):
+                    cum += e[i] / e.sum()
+                    if cum <= 1.0 - top_p:
+                        keep = i
+                    else:
+                        break
+            tk = tk[:keep]
+        else:  # general path: HF TopK (k' = max(top_k, 2), ties kept) then HF TopP (min_keep 2)
+            keep_m = np.isfinite(s)
+            if top_k > 0:
+                keep_m &= s >= s[order[max(top_k, 2) - 1]]
+            if top_p < 1.0:
+                asc = np.argsort(np.where(keep_m, s, -np.inf), kind="stable")
+                sv = np.where(keep_m, s, -np.inf)[asc].astype(np.float64)
+                pr = np.exp(sv - sv.max())
+                cum = np.cumsum(pr / pr.sum())
+                rem = cum <= 1.0 - top_p
+                rem[-2:] = False
+                keep_m[asc[rem]] = False
+            tk = [int(t) for t in order if keep_m[t]]
         rkey = _mix64(seed ^ _mix64((((r + row0) & 0xFFFFFFFF) << 32) | col))
         score = np.array([s[t] + bscore[r] for t in tk])
         key = np.array([score[i] + _gumbel(rkey + t + 1) for i, t in enumerate(tk)])
