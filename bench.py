@@ -214,10 +214,11 @@ def main():
     ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c3",
                     help="BASELINE.json configs: c3 (default, the metric's config: batch 32 per GPU), c2 (one "
                          "utterance), c5 (srt_dubbing long-form: a synthetic SRT of --cues cues sharded over the "
-                         "ranks, length-bucketed chunks of 32 streamed through the pipelined driver)")
+                         "ranks, each rank's cue loop calling IndexTTS.infer per cue)")
     ap.add_argument("--cues", type=int, default=256)
-    ap.add_argument("--chunk", type=int, default=128,
-                    help="C5: rows per decode chunk (the product's long-form chunk, IndexTTS.LONGFORM_BATCH)")
+    ap.add_argument("--c5-decoding", choices=("srt", "greedy"), default="srt",
+                    help="C5: srt_dubbing's own decoding (the reference defaults its engine leaves in place) "
+                         "or greedy")
     ap.add_argument("--decoding", choices=("greedy", "beam3"), default="greedy",
                     help="greedy (the headline) or beam3: the reference's default production decoding "
                          "(do_sample=True, num_beams=3, top_k=30, top_p=0.8, infer.py:535-543), 3 beam rows "
@@ -248,13 +249,13 @@ def main():
     from indextts.utils.synthetic import bigvgan_state_dict, gpt_state_dict
 
     cfg = load_config(default_config_path())
+    if args.workload == "c5":
+        return long_form(args, cfg, dev, world, rank)
     gsd = gpt_state_dict(cfg.gpt, seed=0, mel_head_std=0.08)
     vsd = bigvgan_state_dict(cfg.bigvgan, seed=0)
     if args.workload == "c2":
         args.batch = 1
     B, N, L = args.batch, args.codes, args.text_len
-    if args.workload == "c5":
-        return long_form(args, cfg, gsd, vsd, dev, world, rank)
     tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + L + 2 + 1 + N + 8)
     timer, t_act, t_amp = KernelTimer(), KernelTimer(), KernelTimer()
     install_conv_timer(tts.vocoder, timer)
@@ -368,6 +369,9 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic: seeded random-init IndexTTS-1.5 weights, random 511-frame prompt mels, random text ids",
+        # the driver's contract: value = the whole-job aggregate over all ranks (the metric's "/GPU" is
+        # per_gpu_value; at N = 1 they coincide)
+        "value_is": "whole-job aggregate over all GPUs; per_gpu_value = value / n_gpus",
         "per_gpu_value": round(audio / dt / world, 3),
         "decoding": "greedy" if args.decoding == "greedy" else "beam sample, num_beams=3, top_k=30, top_p=0.8",
         "config": {"workload": f"{'C2' if args.workload == 'c2' else 'C3'}: batch={B} zero-shot utterance"
@@ -385,47 +389,80 @@ def main():
         dist.destroy_process_group()
 
 
-def long_form(args, cfg, gsd, vsd, dev, world, rank):
-    """C5 (BASELINE.json configs[4]): srt_dubbing long-form.  A synthetic SRT of args.cues cues (seed 3),
-    cue text L ~ U[8, 96], one shared prompt (features computed once, cached by key); cue i runs on rank
-    i % world; each rank sorts its cues by length into chunks of args.chunk (default 128, the product's
-    long-form chunk: IndexTTS.LONGFORM_BATCH; the decode ids padded to the chunk's
-    bucket with the stop id 1 via ``pad_to`` -- prepare_gpt_inputs strips it, the latent pass gets the
-    unpadded ids: per-cue results are unchanged), 6 codes per text token of the bucket (EOS
-    suppressed), and streams the chunks through the pipelined driver;
-    the finished waveforms are gathered to rank 0.  One step = the whole SRT."""
-    from indextts.pipeline import BatchedTTS, SR
+WORDS = ("mind the gap please stand clear of closing doors there is a vehicle arriving in dock next station "
+         "last stop change here for northern line thank you travelling with us take all your belongings "
+         "this train terminates platform passengers are reminded to keep their luggage with them").split()
+
+
+def synthetic_srt(tokenizer, n_cues, seed=3):
+    """C5's synthetic SRT: n_cues cue texts of L ~ U[8, 96] BPE tokens each (seeded words)."""
+    g = np.random.default_rng(seed)
+    texts = []
+    for L in g.integers(8, 97, n_cues):
+        words = []
+        while len(tokenizer.tokenize(" ".join(words))) < L:
+            words.append(WORDS[int(g.integers(len(WORDS)))])
+        texts.append(" ".join(words).capitalize() + ".")
+    return texts
+
+
+def _write_prompt_wav(path, seconds=5.0, sr=24000, seed=3):
+    import wave
+    g = np.random.default_rng(seed)
+    t = np.arange(int(seconds * sr)) / sr
+    sig = 0.3 * np.sin(2 * np.pi * (140 + 60 * np.sin(2 * np.pi * 0.7 * t)) * t) + 0.03 * g.standard_normal(t.size)
+    with wave.open(path, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(sr)
+        w.writeframes((sig * 32767).astype("<i2").tobytes())
+
+
+class _Cue:  # srt_parser.SRTEntry's fields the strategies read
+    def __init__(self, index, text):
+        self.index, self.text, self.duration = index, text, 0.0
+
+
+def long_form(args, cfg, dev, world, rank):
+    """C5 (BASELINE.json configs[4]): srt_dubbing long-form THROUGH THE DROP-IN API.  A synthetic SRT of
+    args.cues cues (L ~ U[8, 96] tokens, seed 3) and one prompt wav; a synthetic IndexTTS-1.5
+    checkpoint directory in the reference's layout (seeded weights) loaded by ``IndexTTS(cfg_path,
+    model_dir, is_fp16=True)`` as srt_dubbing's IndexTTSEngine builds it; per rank, cue i (i % world ==
+    rank) is synthesised by BasicStrategy's loop -- ``for i, entry in enumerate(entries):
+    infer(text=entry.text, audio_prompt=voice, output_path=None, **filtered)``
+    (srt_dubbing/src/strategies/basic_strategy.py:65-74, tts_engines/index_tts_engine.py:45-63).  The
+    cue lookahead batches the loop (chunks of LONGFORM_BATCH rows; with ITTS_DEVICES a single process
+    deals them over several GPUs); the finished int16 waveforms are gathered to rank 0 over RCCL.
+    --c5-decoding srt: srt_dubbing's decoding = the reference defaults (IndexTTSEngine's
+    inspect.signature filter drops every decoding kwarg, Q9: beam sample, num_beams 3, top_k 30,
+    top_p 0.8, max_mel_tokens 600); greedy: do_sample=False, num_beams=1.  One step = the whole SRT."""
+    import tempfile
+    from indextts.infer import IndexTTS
+    from indextts.pipeline import SR
     from indextts.sharding import gather_waveforms, shard
-    g = np.random.default_rng(3)
-    n_cues = args.cues
-    lens_all = g.integers(8, 97, n_cues)
-    texts_all = [torch.from_numpy(g.integers(2, int(cfg.gpt.number_text_tokens), int(n)).astype(np.int64))
-                 for n in lens_all]
-    mel = torch.from_numpy(g.normal(-4.0, 2.0, (1, 100, args.prompt_frames)).astype(np.float32)).to(dev)
-    buckets = (32, 64, 96)
-    tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + 96 + 2 + 1 + 6 * 96 + 8)
-    mine = sorted(shard(n_cues, world, rank), key=lambda i: -int(lens_all[i]))
-    batches, keys, order = [], [], []
-    for c in range(0, len(mine), args.chunk):
-        idx = mine[c: c + args.chunk]
-        order += idx
-        bl = next(b for b in buckets if b >= max(int(lens_all[i]) for i in idx))
-        tx = [texts_all[i].to(dev) for i in idx]
-        batches.append(([mel] * len(idx), tx, {"max_mel_tokens": 6 * bl, "min_new_tokens": 6 * bl, "pad_to": bl}))
-        keys.append([("prompt", 0)] * len(idx))
+    from indextts.utils.synthetic import write_checkpoint_dir
+    root = os.environ.get("ITTS_BENCH_CKPT") or os.path.join(tempfile.gettempdir(), "itts_bench_ckpt")
+    if rank == 0:
+        write_checkpoint_dir(root, cfg, os.path.join(REPO, "tests", "golden", "tiny_bpe.model"), seed=0,
+                             mel_head_std=0.08)
+        _write_prompt_wav(os.path.join(root, "voice.wav"))
+    if world > 1:
+        dist.barrier()
+    voice = os.path.join(root, "voice.wav")
+    tts = IndexTTS(cfg_path=os.path.join(root, "config.yaml"), model_dir=root, is_fp16=True, device=str(dev))
+    texts = synthetic_srt(tts.tokenizer, args.cues)
+    mine = shard(len(texts), world, rank)
+    entries = [_Cue(i + 1, texts[i]) for i in mine]
+    kw = {} if args.c5_decoding == "srt" else dict(do_sample=False, num_beams=1)
 
     def step():
-        res = tts.synthesize_many(batches, keys=keys)
-        torch.cuda.synchronize()
-        audio = 0.0
-        by_cue = {}
-        it = iter(order)
-        for pcm, lens, _ in res:
-            for b in range(pcm.shape[0]):
-                by_cue[next(it)] = pcm[b, : int(lens[b])]
-            audio += float(lens.sum()) / SR
+        pcm = []
+        for i, entry in enumerate(entries):  # BasicStrategy.process_entries (engine filters kwargs: Q9)
+            _, data = tts.infer(text=entry.text, audio_prompt=voice, output_path=None, **kw)
+            pcm.append(torch.from_numpy(data.reshape(-1)))
+        audio = sum(float(p.numel()) for p in pcm) / SR
         if world > 1:  # in this rank's shard order
-            gather_waveforms([by_cue[i] for i in shard(n_cues, world, rank)], n_cues, dev)
+            gather_waveforms([p.to(dev) for p in pcm], len(texts), dev)
         return audio
 
     for _ in range(args.warmup):
@@ -448,17 +485,26 @@ def long_form(args, cfg, gsd, vsd, dev, world, rank):
         a = torch.tensor([audio], device=dev, dtype=torch.float64)
         dist.all_reduce(a, op=dist.ReduceOp.SUM)
         audio = float(a)
+    ndev = tts.n_devices
+    tts.close()
     if rank == 0:
+        dec = ("srt_dubbing's decoding (reference defaults: beam sample, num_beams=3, top_k=30, top_p=0.8, "
+               "max_mel_tokens=600)" if args.c5_decoding == "srt" else "greedy, max_mel_tokens=600")
         print(json.dumps({
-            "metric": METRIC, "value": round(audio / dt, 3), "unit": "audio-seconds/sec", "n_gpus": world,
+            "metric": METRIC, "value": round(audio / dt, 3), "unit": "audio-seconds/sec", "n_gpus": world * ndev,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic: seeded random-init IndexTTS-1.5 weights, one random 511-frame prompt mel, "
-                    "random cue text ids",
-            "config": {"workload": f"C5: srt long-form, {n_cues} cues (L ~ U[8,96]) sharded over {world} GPU(s), "
-                                   f"length-bucketed chunks of {args.chunk} (buckets 32/64/96 text ids, 6 codes per id: <= 600 = max_mel_tokens), "
-                                   "pipelined decode || latent+vocoder, RCCL gather",
-                       "global_batch": n_cues, "seq_len": None, "parallelism": f"dp{world}"}}), flush=True)
+            "value_is": "whole-job aggregate over all GPUs; per_gpu_value = value / n_gpus",
+            "per_gpu_value": round(audio / dt / (world * ndev), 3), "audio_seconds": round(audio / args.steps, 2),
+            "data": "synthetic: seeded random-init IndexTTS-1.5 checkpoint directory, one 5 s prompt wav, "
+                    "synthetic SRT cue texts (tiny BPE)",
+            "decoding": dec,
+            "config": {"workload": f"C5: srt long-form, {len(texts)} cues (L ~ U[8,96] tokens) through "
+                                   f"IndexTTS.infer per cue (BasicStrategy loop; cue lookahead batching, "
+                                   f"chunks of {IndexTTS.LONGFORM_BATCH} rows), sharded over {world} rank(s) x "
+                                   f"{ndev} device(s) per rank, RCCL gather",
+                       "global_batch": len(texts), "seq_len": None, "parallelism": f"dp{world * ndev}"}}),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -307,241 +307,6 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
   }
 }
 
-// ---- split-S decode attention (flash-decoding partials, last-arriver merge) ---------------------
-// The keys of one (head, sequence) are cut into chunks of `chunk` keys (chunk = rounds * NG * KB);
-// workgroup (h, b, s) runs chunk s exactly as attn_decode_kernel runs the whole range (same 8-lane
-// groups, online softmax, fixed-order LDS merge) and ends with the chunk's (max M_s, sum L_s,
-// unnormalised o_s[64]).  With one active chunk it writes the output itself.  Otherwise it publishes
-// its partial to ws[b][h][s][72] with write-through (sc1) stores, every storing wave drains them
-// (s_waitcnt vmcnt(0)), the workgroup barrier, then one lane adds 1 to the (b, h) counter (agent
-// scope) -- the workgroup whose add returns n_act - 1 is the last: it resets the counter, reads every
-// partial with sc1 loads and merges them in chunk order (M = max M_s, L = sum L_s e^(M_s - M),
-// o = sum o_s e^(M_s - M) / L): deterministic, and the chunking depends only on the sequence's own
-// key count (batch-invariant).  MI355X_MICROARCH.md "Valid forms", first row of the sc1 table.
-// Partial lines of one (b, h) are read once per launch, by its last arriver only, so no XCD L2 holds
-// a stale copy within a launch (kernel boundaries write back / invalidate the L2s).
-// Why: one workgroup per (head, row) puts 2 workgroups of ~72 KiB of K/V each on a CU and its
-// single round of loads leaves the CU idle while the merge and the output run; chunks spread the
-// same bytes over 4x the workgroups.
-constexpr int kWsPitch = 72;  // floats per published partial (64 o + M + L, padded to 16 B)
-
-template <typename TC, typename TO, int NT, int KB, bool ROWS>
-__global__ __launch_bounds__(NT) void attn_split_kernel(const float* __restrict__ qkv, int64_t ldqkv,
-                                                        const float* __restrict__ qkv_bias, TC* __restrict__ cache_k,
-                                                        TC* __restrict__ cache_v, int64_t cache_bs, int64_t cache_hs,
-                                                        const int32_t* pad, int kv_base,
-                                                        const int32_t* __restrict__ tstate, TO* __restrict__ out,
-                                                        int64_t ldo, int H, const int32_t* __restrict__ kv_rows,
-                                                        int64_t ld_rows, float* ws, int* cnt, int chunk, int nsmax) {
-  constexpr int NG = NT / 8;
-  constexpr int RW = sizeof(TC) * 8 / 16;
-  __shared__ float qs[kHD], kn[kHD], vn[kHD];
-  __shared__ float gm[NG], gl[NG];
-  __shared__ float pv[NG + NT / kHD + 1][kHD + 1];
-  __shared__ int last_flag;
-  const int h = blockIdx.x, b = blockIdx.y, sp = blockIdx.z;
-  const int D = H * kHD;
-  const int kidx = kv_base + tstate[0];
-  const int p0 = pad ? pad[b] : 0;
-  const int nk = kidx + 1 - p0;
-  const int jlo = sp * chunk;
-  if (jlo >= nk) return;  // chunk beyond this sequence's keys (uniform over the workgroup)
-  const int jhi = min(nk, jlo + chunk);
-  const int n_act = (nk + chunk - 1) / chunk;
-  const bool own_last = jhi == nk;  // holds this step's key: appends it to the cache
-  TC* Kc = cache_k + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
-  TC* Vc = cache_v + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
-  const int32_t* rows = ROWS ? kv_rows + (int64_t)b * ld_rows : nullptr;
-  auto koff = [&](int p) -> int64_t {
-    if constexpr (ROWS) return (int64_t)(rows[p] - b) * cache_bs + (int64_t)p * kHD;
-    else return (int64_t)p * kHD;
-  };
-  const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
-  const bool qkv_lane = threadIdx.x < 3 * kHD;
-  const int which = threadIdx.x / kHD, dq = threadIdx.x - which * kHD;
-  const int col = which * D + h * kHD + dq;
-  float qv = 0.f;
-  if (qkv_lane && (which == 0 || own_last)) qv = qkv[(int64_t)b * ldqkv + col] + (qkv_bias ? qkv_bias[col] : 0.f);
-  u32x4_t kr[KB][RW], vr[KB][RW];
-  const int jclamp = max(nk - 2, 0);
-  auto kv_load = [&](u32x4_t (&dst)[KB][RW], const TC* base, int j0) {
-#pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      const int j = min(j0 + NG * u + g, jclamp);
-#pragma unroll
-      for (int w = 0; w < RW; ++w) {
-        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(base + koff(p0 + j) + 8 * d8) + w;
-#if ITTS_KV_NT
-        dst[u][w] = __builtin_nontemporal_load(src);
-#else
-        dst[u][w] = *src;
-#endif
-      }
-    }
-  };
-  kv_load(kr, Kc, jlo);
-  kv_load(vr, Vc, jlo);
-  if (qkv_lane) {
-    if (which == 0) {
-      qs[dq] = qv * 0.125f;
-    } else if (own_last) {
-      if (which == 1) {
-        kn[dq] = qv;
-        St<TC>::st(Kc + (int64_t)kidx * kHD + dq, qv);
-      } else {
-        vn[dq] = qv;
-        St<TC>::st(Vc + (int64_t)kidx * kHD + dq, qv);
-      }
-    }
-  }
-  __syncthreads();
-  float q[8], kme[8], vme[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    q[e] = qs[8 * d8 + e];
-    kme[e] = own_last ? kn[8 * d8 + e] : 0.f;
-    vme[e] = own_last ? vn[8 * d8 + e] : 0.f;
-  }
-  auto unpack = [&](const u32x4_t (&r)[RW], float (&x)[8]) {
-    if constexpr (sizeof(TC) == 2) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        x[2 * i] = __uint_as_float(r[0][i] << 16);
-        x[2 * i + 1] = __uint_as_float(r[0][i] & 0xFFFF0000u);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = __uint_as_float(r[i / 4][i % 4]);
-    }
-  };
-  float m = -INFINITY, l = 0.f;
-  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j0 = jlo; j0 < jhi; j0 += NG * KB) {
-    const bool more = j0 + NG * KB < jhi;
-    float s[KB];
-    float bm = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      const int j = j0 + NG * u + g;
-      float kx[8];
-      unpack(kr[u], kx);
-      if (j >= nk - 1) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) kx[e] = kme[e];
-      }
-      float pt = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) pt = fmaf(q[e], kx[e], pt);
-      pt = sum8_dpp(pt);
-      s[u] = j < jhi ? pt : -INFINITY;
-      bm = fmaxf(bm, s[u]);
-    }
-    if (more) kv_load(kr, Kc, j0 + NG * KB);
-    if (bm != -INFINITY) {
-      const float mn = fmaxf(m, bm);
-      const float corr = __expf(m - mn);
-      l *= corr;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] *= corr;
-#pragma unroll
-      for (int u = 0; u < KB; ++u) {
-        const int j = j0 + NG * u + g;
-        const float pr = __expf(s[u] - mn);
-        l += pr;
-        float vx[8];
-        unpack(vr[u], vx);
-        if (j >= nk - 1) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) vx[e] = vme[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = fmaf(pr, vx[e], o[e]);
-      }
-      m = mn;
-    }
-    if (more) kv_load(vr, Vc, j0 + NG * KB);
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) pv[g][8 * d8 + e] = o[e];
-  if (d8 == 0) {
-    gm[g] = m;
-    gl[g] = l;
-  }
-  __syncthreads();
-  constexpr int NQ = NT / kHD, GPQ = NG / NQ;
-  float* qsum = &pv[0][0] + NG * (kHD + 1);
-  float* lsum = qsum + NQ * (kHD + 1);
-  float M = -INFINITY;
-  {
-    const int dd = threadIdx.x & (kHD - 1), qd = threadIdx.x / kHD;
-#pragma unroll 8
-    for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
-    float L = 0.f, acc = 0.f;
-#pragma unroll
-    for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
-      const float w = __expf(gm[i] - M);
-      L = fmaf(gl[i], w, L);
-      acc = fmaf(pv[i][dd], w, acc);
-    }
-    qsum[qd * (kHD + 1) + dd] = acc;
-    if (dd == 0) lsum[qd] = L;
-  }
-  __syncthreads();
-  float L = 0.f, acc = 0.f;
-  if (threadIdx.x < kHD) {
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      L += lsum[i];
-      acc += qsum[i * (kHD + 1) + threadIdx.x];
-    }
-  }
-  if (n_act == 1) {
-    if (threadIdx.x < kHD) St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, acc / L);
-    return;
-  }
-  float* wsp = ws + (((int64_t)b * H + h) * nsmax) * kWsPitch;
-  if (threadIdx.x < kHD) {
-    __hip_atomic_store(wsp + sp * kWsPitch + threadIdx.x, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) {
-      __hip_atomic_store(wsp + sp * kWsPitch + kHD, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(wsp + sp * kWsPitch + kHD + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  int* c = cnt + (int64_t)b * H + h;
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_flag = old == n_act - 1;
-    if (old == n_act - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!last_flag || threadIdx.x >= kHD) return;
-  float Ms[8], Ls[8], As[8];  // n_act <= nsmax <= 8 (host-checked)
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    if (s < n_act) {
-      const float* src = wsp + s * kWsPitch;
-      As[s] = __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      Ms[s] = __hip_atomic_load(src + kHD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      Ls[s] = __hip_atomic_load(src + kHD + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  float MM = -INFINITY;
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < n_act) MM = fmaxf(MM, Ms[s]);
-  float LL = 0.f, AA = 0.f;
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < n_act) {
-      const float w = __expf(Ms[s] - MM);
-      LL = fmaf(Ls[s], w, LL);
-      AA = fmaf(As[s], w, AA);
-    }
-  St<TO>::st(out + (int64_t)b * ldo + h * kHD + threadIdx.x, AA / LL);
-}
-
 constexpr int kQB = 128;  // queries per workgroup (one per thread)
 constexpr int kKB = 32;   // keys per LDS block
 
@@ -854,55 +619,6 @@ extern "C" int itts_attn_decode_proj(const float* qkv, int64_t ldqkv, int nsplit
   return attn_decode_launch(fn, qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v, cache_bs, cache_hs,
                             smax, pad, kv_base, tstate, nullptr, 0, B, H, cache_dtype, ITTS_F32, kv_rows, ld_rows,
                             w_proj, N, part, part_stride, ldp, stream);
-}
-
-#ifndef ITTS_ASPLIT_NT
-#define ITTS_ASPLIT_NT 256
-#endif
-#ifndef ITTS_ASPLIT_KB
-#define ITTS_ASPLIT_KB 3
-#endif
-extern "C" int itts_attn_split_params(int* nt, int* kb) {
-  if (nt) *nt = ITTS_ASPLIT_NT;
-  if (kb) *kb = ITTS_ASPLIT_KB;
-  return ITTS_ASPLIT_NT / 8 * ITTS_ASPLIT_KB;  // keys per round of one workgroup
-}
-
-extern "C" int itts_attn_decode_split(const float* qkv, int64_t ldqkv, const float* qkv_bias, void* cache_k,
-                                      void* cache_v, int64_t cache_bs, int64_t cache_hs, int smax, const int32_t* pad,
-                                      int kv_base, const int32_t* tstate, void* out, int64_t ldo, int B, int H,
-                                      int cache_dtype, int out_dtype, const int32_t* kv_rows, int64_t ld_rows,
-                                      float* ws, int* cnt, int chunk, void* stream) {
-  const char* fn = "itts_attn_decode_split";
-  ITTS_REQUIRE(B >= 0 && H > 0, fn, "bad sizes");
-  if (B == 0) return 0;
-  ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && out && ws && cnt, fn, "null pointer");
-  ITTS_REQUIRE(smax <= kMaxKeys && cache_hs >= (int64_t)smax * kHD, fn, "bad cache capacity");
-  ITTS_REQUIRE(!kv_rows || ld_rows >= smax, fn, "kv_rows [B][ld_rows >= smax] required");
-  ITTS_REQUIRE(chunk > 0 && (chunk % (ITTS_ASPLIT_NT / 8 * ITTS_ASPLIT_KB)) == 0, fn,
-               "chunk must be a multiple of the keys per round (itts_attn_split_params)");
-  const int nsmax = (smax + chunk - 1) / chunk;
-  ITTS_REQUIRE(nsmax <= 8, fn, "at most 8 chunks per sequence: raise chunk");
-  dim3 grid(H, B, nsmax);
-  hipStream_t s = itts::as_stream(stream);
-  constexpr int NT = ITTS_ASPLIT_NT, KB = ITTS_ASPLIT_KB;
-#define ITTS_AS(TC, TO)                                                                                             \
-  do {                                                                                                              \
-    if (kv_rows)                                                                                                    \
-      hipLaunchKernelGGL((attn_split_kernel<TC, TO, NT, KB, true>), grid, dim3(NT), 0, s, qkv, ldqkv, qkv_bias,     \
-                         (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base, tstate, (TO*)out, ldo, H,      \
-                         kv_rows, ld_rows, ws, cnt, chunk, nsmax);                                                  \
-    else                                                                                                            \
-      hipLaunchKernelGGL((attn_split_kernel<TC, TO, NT, KB, false>), grid, dim3(NT), 0, s, qkv, ldqkv, qkv_bias,    \
-                         (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base, tstate, (TO*)out, ldo, H,      \
-                         nullptr, 0, ws, cnt, chunk, nsmax);                                                        \
-  } while (0)
-  if (cache_dtype == ITTS_BF16 && out_dtype == ITTS_BF16) ITTS_AS(uint16_t, uint16_t);
-  else if (cache_dtype == ITTS_F32 && out_dtype == ITTS_F32) ITTS_AS(float, float);
-  else if (cache_dtype == ITTS_BF16) ITTS_AS(uint16_t, float);
-  else ITTS_AS(float, uint16_t);
-#undef ITTS_AS
-  return itts::check_launch(fn);
 }
 
 extern "C" int itts_attn_decode_rows(const float* qkv, int64_t ldqkv, int nsplit, int64_t split_stride,

@@ -31,6 +31,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+from .devpool import DevicePool, WorkerError, deal, parse_devices
 from .pipeline import HOP, SR, BatchedTTS, remove_long_silence as _rls_row
 from .utils.audio import prompt_mel, save_wav_int16
 from .utils.config import load_config
@@ -48,27 +49,36 @@ def _load_state_dict(path: str, key: Optional[str] = None) -> Dict[str, torch.Te
     return sd
 
 
+def _is_cue_list(v) -> bool:
+    return isinstance(v, (list, tuple)) and len(v) > 1 and all(
+        isinstance(getattr(e, "text", None), str) for e in v[:8])
+
+
 def _caller_cue_texts(text: str, max_depth: int = 8) -> Optional[List[str]]:
-    """The texts of the cues from ``text`` on, when ``infer`` runs inside a loop over a cue list:
+    """FALLBACK discovery of the caller's cue list (the explicit hook is ``IndexTTS.prefetch``): the
+    texts of the cues from ``text`` on, when ``infer`` runs inside a loop over a list of cue objects.
     srt_dubbing's strategies iterate ``for i, entry in enumerate(entries)`` and call
-    ``tts_engine.synthesize(text=entry.text, ...)`` (srt_dubbing/src/strategies/basic_strategy.py:64-72,
+    ``tts_engine.synthesize(text=entry.text, ...)`` (srt_dubbing/src/strategies/basic_strategy.py:65-74,
     stretch / hq_stretch / adaptive likewise) -> ``IndexTTSEngine.synthesize`` -> ``infer``
-    (tts_engines/index_tts_engine.py:45-58).  Found by looking for a local ``entries`` list of objects
-    with a ``text`` attribute in the calling frames; None when there is no such loop."""
+    (tts_engines/index_tts_engine.py:45-63).  In each calling frame (innermost first) any local list
+    or tuple of objects with a ``str`` ``text`` attribute that contains ``text`` is a candidate (the one
+    named ``entries`` first); the caller's position is an ``int`` local that indexes a cue with this
+    text (the loop counter, whatever its name), else the first cue with this text.  None when no frame
+    holds such a list: then ``infer`` synthesises this text alone, exactly as the reference does."""
     f = sys._getframe(2)
     try:
         for _ in range(max_depth):
             if f is None:
                 return None
-            ents = f.f_locals.get("entries")
-            if isinstance(ents, (list, tuple)) and ents and all(hasattr(e, "text") for e in ents[:8]):
-                texts = [str(e.text) for e in ents]
-                i = f.f_locals.get("i")
-                if isinstance(i, int) and 0 <= i < len(texts) and texts[i] == text:
-                    return texts[i:]
-                if text in texts:
-                    return texts[texts.index(text):]
-                return None
+            loc = f.f_locals
+            cands = sorted(((n != "entries", n) for n, v in loc.items() if _is_cue_list(v)))
+            for _, name in cands:
+                texts = [e.text for e in loc[name]]
+                if text not in texts:
+                    continue
+                pos = next((v for v in loc.values() if type(v) is int and 0 <= v < len(texts) and texts[v] == text),
+                           None)
+                return texts[texts.index(text) if pos is None else pos:]
             f = f.f_back
         return None
     finally:
@@ -92,6 +102,16 @@ class IndexTTS:
             raise RuntimeError(f"device {device!r}: the MI355X build runs on HIP devices ('cuda[:n]') only")
         self.device = str(device)
         self.is_fp16 = bool(is_fp16)
+        # more GPUs behind this one object (ITTS_DEVICES="0,1,..." or "all"): worker processes are
+        # spawned first so that they load their weights while this process builds its own engine
+        self._pool = None
+        workers = parse_devices(os.environ.get("ITTS_DEVICES"), torch.cuda.device_count())
+        if self.device in workers:
+            workers.remove(self.device)  # this process is the listed device's engine
+        elif workers and self.device == "cuda" and "cuda:0" in workers:
+            workers.remove("cuda:0")
+        if workers:
+            self._pool = DevicePool(cfg_path, model_dir, self.is_fp16, workers)
         # the fused anti-alias activation is always the HIP kernel here; kept for API compatibility
         self.use_cuda_kernel = use_cuda_kernel is None or bool(use_cuda_kernel)
         self.cfg = load_config(cfg_path)
@@ -333,60 +353,188 @@ class IndexTTS:
         strategies -> ``IndexTTSEngine.synthesize``, unchanged): a result prefetched by ``prefetch``
         (or by the lookahead below) for the same prompt, text and arguments is returned instead of a
         new synthesis."""
-        hit = self._take_ahead(audio_prompt, text, max_text_tokens_per_sentence, generation_kwargs)
-        if hit is None and self.LOOKAHEAD > 0:
+        key = self._ahead_key(audio_prompt, max_text_tokens_per_sentence, generation_kwargs)
+        hit = self._take_ahead(key, text)
+        if hit is None and self._lookahead_ok(key, text):
             upcoming = _caller_cue_texts(text)
             if upcoming and len(upcoming) > 1:
-                self.prefetch(audio_prompt, upcoming[: self.LOOKAHEAD], max_text_tokens_per_sentence,
-                              **generation_kwargs)
-                hit = self._take_ahead(audio_prompt, text, max_text_tokens_per_sentence, generation_kwargs)
+                window = upcoming[: self.LOOKAHEAD * self.n_devices]
+                try:
+                    self.prefetch(audio_prompt, window, max_text_tokens_per_sentence, **generation_kwargs)
+                except Exception as e:  # noqa: BLE001 -- e.g. one bad cue: never fail the whole window
+                    # its cues are synthesised one call at a time from now on, so an error hits only the
+                    # cue that causes it (the reference's behaviour: basic_strategy.py:86-97 writes silence)
+                    warnings.warn(f"lookahead batch of {len(window)} cues failed ({e!r}); those cues are "
+                                  "synthesised one call at a time", RuntimeWarning)
+                    self._ahead_state()["bad"].update(window)
+                hit = self._take_ahead(key, text)
+        self._ahead_state()["last"] = (text, key)
         if hit is not None:
             return self._deliver(hit, output_path)
         return self._synthesize(audio_prompt, text, output_path, verbose, max_text_tokens_per_sentence,
                                 generation_kwargs, fast=False)
 
     # ------------------------------------------------------------------ cross-call batching
-    # Cues synthesised ahead when ``infer`` is called from inside a loop over a cue list (0: off).
+    # Cues synthesised ahead per device when ``infer`` is called from inside a loop over a cue list
+    # (0: off).  The explicit hook is ``prefetch``; the frame walk (_caller_cue_texts) is the fallback
+    # that batches the unchanged srt_dubbing caller.
     LOOKAHEAD = int(os.environ.get("ITTS_LOOKAHEAD", "128"))
+    AHEAD_CAP_WINDOWS = 4  # prefetched results kept: at most this many windows (oldest dropped)
+
+    @property
+    def n_devices(self) -> int:
+        return 1 + (len(self._pool.alive()) if self.__dict__.get("_pool") is not None else 0)
+
+    def _ahead_state(self):
+        st = self.__dict__.get("_ahead_st")
+        if st is None:
+            # ahead: (key, text) -> FIFO of results; win: key -> [issued, consumed] of its last window;
+            # recent: keys of the last windows, oldest first; bad: texts of windows that failed;
+            # last: (text, key) of the previous call
+            st = self.__dict__["_ahead_st"] = {"ahead": {}, "win": {}, "recent": [], "bad": set(), "last": None}
+        return st
+
+    @property
+    def _ahead(self):
+        return self._ahead_state()["ahead"]
 
     def _ahead_key(self, audio_prompt, max_tokens, gen):
+        """None for a prompt that is not a path (no cross-call reuse: an object's id can be recycled)."""
+        if not isinstance(audio_prompt, str):
+            return None
         try:
-            mtime = os.path.getmtime(audio_prompt) if isinstance(audio_prompt, str) else None
+            mtime = os.path.getmtime(audio_prompt)
         except OSError:
             mtime = None
-        prompt = audio_prompt if isinstance(audio_prompt, str) else id(audio_prompt)
-        return (prompt, mtime, int(max_tokens), tuple(sorted((k, repr(v)) for k, v in gen.items())))
+        return (audio_prompt, mtime, int(max_tokens), tuple(sorted((k, repr(v)) for k, v in gen.items())))
 
-    def _take_ahead(self, audio_prompt, text, max_tokens, gen):
-        ahead = self.__dict__.setdefault("_ahead", {})
-        q = ahead.get((self._ahead_key(audio_prompt, max_tokens, gen), text))
+    def _lookahead_ok(self, key, text) -> bool:
+        """Batch ahead only for a stable argument set: not for a path-less prompt, not for a text whose
+        window failed, not when the same text was just requested with other arguments (a duration
+        search varying length_penalty per attempt: each attempt is one call, as in the reference), and
+        not once the last three windows went mostly unused (< 1/4 of their results taken)."""
+        st = self._ahead_state()
+        if key is None or self.LOOKAHEAD <= 0 or text in st["bad"] or st.get("off_all"):
+            return False
+        last = st["last"]
+        if last is not None and last[0] == text and last[1] != key:
+            return False
+        recent = [st["win"][k] for k in st["recent"][-3:] if k in st["win"]]
+        if len(recent) == 3 and all(w[0] >= 4 and 4 * w[1] < w[0] for w in recent):
+            # the last three windows went mostly unused (a caller that changes its arguments per cue):
+            # batching ahead only multiplies the work -- off for this object from now on
+            warnings.warn("cue lookahead switched off: prefetched results went unused", RuntimeWarning)
+            st["off_all"] = True
+            return False
+        return True
+
+    def _take_ahead(self, key, text):
+        if key is None:
+            return None
+        st = self._ahead_state()
+        q = st["ahead"].get((key, text))
         if not q:
             return None
         res = q.pop(0)  # one result per call: a repeated call synthesises anew (new draws when sampling)
         if not q:
-            del ahead[(self._ahead_key(audio_prompt, max_tokens, gen), text)]
+            del st["ahead"][(key, text)]
+        w = st["win"].get(key)
+        if w is not None:
+            w[1] += 1
         return res
 
     def prefetch(self, audio_prompt, texts, max_text_tokens_per_sentence=120, **generation_kwargs):
-        """Synthesise ``texts`` now, all sentences of all texts batched (``infer_many``), and keep one
-        result per occurrence for the ``infer`` calls that follow with the same prompt, text and
+        """Synthesise ``texts`` now, all sentences of all texts batched (``infer_many``; with
+        ITTS_DEVICES, dealt over this process's GPU and the worker GPUs), and keep one result per
+        occurrence for the ``infer`` calls that follow with the same prompt (a path), text and
         arguments.  Deterministic decoding (``do_sample=False``): each result equals what that
-        ``infer`` call would have computed (rows never interact; tests/test_gpu_lookahead.py); with
-        sampling it is an independent draw from the same distribution, as a fresh call would be."""
-        ahead = self.__dict__.setdefault("_ahead", {})
-        base = self._ahead_key(audio_prompt, max_text_tokens_per_sentence, generation_kwargs)
+        ``infer`` call would have computed (rows never interact; tests/test_gpu_lookahead.py,
+        tests/test_gpu_devpool.py); with sampling it is an independent draw from the same
+        distribution, as a fresh call would be.  Results of an earlier window for the same arguments
+        that the caller has moved past are dropped."""
+        key = self._ahead_key(audio_prompt, max_text_tokens_per_sentence, generation_kwargs)
+        if key is None:
+            return
+        st = self._ahead_state()
+        ahead = st["ahead"]
+        window = set(texts)
+        for k in [k for k in ahead if k[0] == key and k[1] not in window]:
+            del ahead[k]  # behind the caller
         need, have = [], {}
         for t in texts:
-            have[t] = have.get(t, len(ahead.get((base, t), [])))
+            if t in st["bad"]:
+                continue
+            have[t] = have.get(t, len(ahead.get((key, t), [])))
             if have[t] > 0:
                 have[t] -= 1
             else:
                 need.append(t)
         if not need:
             return
-        for t, r in zip(need, self.infer_many(audio_prompt, need, None, False, max_text_tokens_per_sentence,
-                                              **generation_kwargs)):
-            ahead.setdefault((base, t), []).append(r)
+        res = self._infer_many_devices(audio_prompt, need, max_text_tokens_per_sentence, generation_kwargs)
+        for t, r in zip(need, res):
+            ahead.setdefault((key, t), []).append(r)
+        st["win"][key] = [len(need), 0]
+        st["recent"] = [k for k in st["recent"] if k != key][-7:] + [key]
+        for k in [k for k in st["win"] if k not in st["recent"]]:
+            del st["win"][k]
+        cap = self.AHEAD_CAP_WINDOWS * max(self.LOOKAHEAD, 1) * self.n_devices
+        while sum(len(q) for q in ahead.values()) > cap:
+            del ahead[next(iter(ahead))]  # oldest first
+
+    def _infer_many_devices(self, audio_prompt, texts, max_tokens, gen):
+        """``infer_many`` over this process's engine and the live workers (longest texts first onto the
+        least-loaded device); a failed worker's share is synthesised here."""
+        pool = self.__dict__.get("_pool")
+        alive = pool.alive() if pool is not None else []
+        if not alive:
+            return self.infer_many(audio_prompt, texts, None, False, max_tokens, **gen)
+        costs = [max(1, len(self.tokenizer.tokenize(t))) for t in texts]
+        bins = deal(costs, 1 + len(alive))
+        tickets = []
+        for wi, share in zip(alive, bins[1:]):
+            if share:
+                try:
+                    tickets.append((share, pool.submit(wi, audio_prompt, [texts[i] for i in share], max_tokens, gen)))
+                except WorkerError:
+                    bins[0] = sorted(bins[0] + share)
+        out = [None] * len(texts)
+        err = None
+        try:
+            if bins[0]:
+                for i, r in zip(bins[0], self.infer_many(audio_prompt, [texts[i] for i in bins[0]], None, False,
+                                                         max_tokens, **gen)):
+                    out[i] = r
+        except Exception as e:  # noqa: BLE001 -- collect the workers' replies first (keeps the pipes in step)
+            err = e
+        redo = []
+        for share, ticket in tickets:
+            try:
+                for i, r in zip(share, pool.result(ticket)):
+                    out[i] = r
+            except WorkerError as e:
+                warnings.warn(f"{e}; its {len(share)} cue(s) are synthesised on {self.device}", RuntimeWarning)
+                redo += share
+        if err is not None:
+            raise err
+        if redo:
+            for i, r in zip(redo, self.infer_many(audio_prompt, [texts[i] for i in redo], None, False, max_tokens,
+                                                  **gen)):
+                out[i] = r
+        return out
+
+    def close(self):
+        """Stop the worker processes (ITTS_DEVICES); also run at interpreter exit."""
+        pool = self.__dict__.get("_pool")
+        if pool is not None:
+            self._pool = None
+            pool.close()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
     @staticmethod
     def _deliver(res, output_path):

@@ -241,3 +241,37 @@ def bigvgan_state_dict(cfg_bv, seed: int = 0) -> Dict[str, np.ndarray]:
         b.normal(f"conds.{i}.weight", (chi, spk, 1), 1.0 / math.sqrt(spk))
         b.normal(f"conds.{i}.bias", (chi,), 0.02)
     return b.sd
+
+
+def _plain(d):
+    if isinstance(d, dict):
+        return {k: _plain(v) for k, v in d.items()}
+    if isinstance(d, list):
+        return [_plain(v) for v in d]
+    return d
+
+
+def write_checkpoint_dir(path: str, cfg, bpe_model: str, seed: int = 0, mel_head_std: float = 0.08,
+                         version: float = 1.5) -> str:
+    """A model directory in the reference's layout (``config.yaml``, ``gpt.pth`` = ``{"model": sd}``,
+    ``bigvgan_generator.pth`` = ``{"generator": sd}``, ``bpe.model``; ``checkpoints/config.yaml:111-113``)
+    holding seeded synthetic weights of ``cfg``'s architecture, so ``IndexTTS(cfg_path, model_dir)``
+    -- and every worker process of an ``ITTS_DEVICES`` pool -- can load it like the real checkpoints.
+    -> path of the config file."""
+    import os
+    import shutil
+
+    import torch
+    import yaml
+    os.makedirs(path, exist_ok=True)
+    cfg = _plain(cfg)
+    cfg["version"] = version
+    with open(os.path.join(path, "config.yaml"), "w") as f:
+        yaml.safe_dump(cfg, f)
+    from .config import AttrDict
+    acfg = AttrDict(cfg)
+    t = lambda sd: {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()}  # noqa: E731
+    torch.save({"model": t(gpt_state_dict(acfg.gpt, seed, mel_head_std))}, os.path.join(path, acfg.gpt_checkpoint))
+    torch.save({"generator": t(bigvgan_state_dict(acfg.bigvgan, seed))}, os.path.join(path, acfg.bigvgan_checkpoint))
+    shutil.copy(bpe_model, os.path.join(path, acfg.dataset["bpe_model"]))
+    return os.path.join(path, "config.yaml")

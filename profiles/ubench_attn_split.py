@@ -1,4 +1,4 @@
-"""Decode attention: one workgroup per (head, row) (itts_attn_decode) vs split-S chunks with a
+"""Decode attention (EXPERIMENT, kernel removed after measurement; it lives in commit 1e046aa): one workgroup per (head, row) (itts_attn_decode) vs split-S chunks with a
 last-arriver merge (itts_attn_decode_split), B = 32 rows, bf16 K/V from HBM (rotating caches),
 hipGraph back-to-back launches.  Also checks the split result against the unsplit one and its
 run-to-run bit identity.  Library from ITTS_HIP_LIB (variant builds: ITTS_ASPLIT_NT / _KB)."""

@@ -88,7 +88,7 @@ def test_lookahead_results_equal_per_call_results(ckpt, tts, monkeypatch):  # no
     assert calls == {"many": 1, "one": 0}, calls
     for i, (g, w) in enumerate(zip(got, want)):
         np.testing.assert_array_equal(g, w, err_msg=f"cue {i}")
-    assert not tts.__dict__.get("_ahead"), "every prefetched result was consumed"
+    assert not tts._ahead, "every prefetched result was consumed"
 
 
 def test_unchanged_srt_dubbing_path_batches(ckpt, tts, monkeypatch):  # noqa: F811
