@@ -164,15 +164,6 @@ int itts_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, int 
  * y = act(acc + bias), 1: y += acc + bias, 2: split-K partials y[ks][m][n] (reduced by
  * itts_residual_reduce_ln).  lnmode 1/2 normalises f32 rows of `a` in the prologue.  c_attn / c_proj /
  * c_fc / mlp.c_proj and mel_head of the KV-cached decode (gpt/model.py:85-192, HF :185-243). */
-/* Split-K residual projection with its reduction inside the launch (bf16 decode, M <= 32 rows):
- * x[M][ldx] += bias + a @ W^T, xh = bf16(x); the split whose arrival completes a 32-column tile sums
- * the ksplit partials (part [ksplit][M][ldp] f32 scratch, split order) -- bit-identical to
- * itts_decode_gemm (epi 2) + itts_residual_reduce_ln without LayerNorm, one launch instead of two.
- * cnt: ceil(N/32) ints, zero before the first launch (every launch leaves them zero).
- * HF modeling_gpt2.py:229-243 (mlp.c_proj) + the residual add of GPT2Block (:300-306). */
-int itts_decode_gemm_reduce(const void* a, int64_t lda, const void* w_packed, int K, int N, int M, const float* bias,
-                            float* part, int64_t ldp, int64_t split_stride, int ksplit, float* x, int64_t ldx, void* xh,
-                            int64_t ldxh, int* cnt, void* stream);
 int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed, int K, int N, int M, const float* bias,
                      const float* g1, const float* b1, const float* g2, const float* b2, int lnmode, int gelu, int epi,
                      void* y, int64_t ldy, int out_dtype, int64_t split_stride, int ksplit, void* stream);

@@ -20,6 +20,8 @@
 //      and the KV lineage table (kv_rows: cache row holding each key position; HF's per-step
 //      _reorder_cache copy of every layer's K/V becomes a copy of 4 B per generated position) --
 //      and writes the next input embedding + ln_1 of each row.
+#include <atomic>
+
 #include "common.h"
 #include "select.h"
 
@@ -728,13 +730,19 @@ extern "C" int itts_beam_select(const float* cand_key, const float* cand_score, 
             hyp_codes, hyp_n, hyp_order, hyp_worst, emb, pos_emb, pos_delta, D, ln_g, ln_b, x, h};
   hipStream_t s = itts::as_stream(stream);
   if (lds_bytes > 64 * 1024) {  // beyond the default dynamic LDS cap (160 KiB per workgroup on gfx950)
-    static const bool once = [] {
+    // per device (the attribute binds to the current device's module), retried until it succeeds
+    static std::atomic<unsigned> raised_mask{0};
+    int dev = 0;
+    ITTS_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 32, fn, "no current HIP device");
+    bool once = (raised_mask.load() >> dev) & 1u;
+    if (!once) {
       const int cap = 144 * 1024;
-      return hipFuncSetAttribute(reinterpret_cast<const void*>(beam_select_kernel<uint16_t>),
+      once = hipFuncSetAttribute(reinterpret_cast<const void*>(beam_select_kernel<uint16_t>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap) == hipSuccess &&
              hipFuncSetAttribute(reinterpret_cast<const void*>(beam_select_kernel<float>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap) == hipSuccess;
-    }();
+      if (once) raised_mask.fetch_or(1u << dev);
+    }
     ITTS_REQUIRE(once, fn, "could not raise the dynamic LDS limit for the reorder buffer");
   }
   if (h_dtype == ITTS_BF16)

@@ -64,14 +64,7 @@ struct DgArgs {
   int gelu;
   void* y;
   int64_t ldy;
-  int64_t split_stride;  // EPI 2/3: floats between the partial products of consecutive K splits
-  // EPI 3 (split-K, the last-arriving split of a column tile reduces): residual x [M][ldx] f32 (+=),
-  // its bf16 copy xh [M][ldxh], one arrival counter per column tile (zero between launches)
-  float* x;
-  int64_t ldx;
-  uint16_t* xh;
-  int64_t ldxh;
-  int* cnt;
+  int64_t split_stride;  // EPI 2: floats between the partial products of consecutive K splits
 };
 
 // normalise RPW rows held in registers (one wave, 64 lanes x KPL elements per row)
@@ -97,14 +90,8 @@ __device__ __forceinline__ void ln_vec(float (&v)[KPL], const float* g, const fl
 }
 
 // EPI: 0 store act(acc + bias) as OutT; 1 f32 Y += acc + bias; 2 split-K over gridDim.y, each split
-// stores its f32 partial product (reduced by a separate launch); 3 split-K with the reduction in the
-// launch: each split publishes its partial with write-through (sc1) stores, every storing wave drains
-// them (s_waitcnt vmcnt(0)), the workgroup barrier, one lane adds to the column tile's counter
-// (agent scope); the split whose add returns nsplit - 1 resets the counter, reads the nsplit partials
-// of its tile with sc1 loads and does x += bias + sum_s partial_s (split order: bit-identical to
-// itts_residual_reduce_ln), xh = bf16(x) -- MI355X_MICROARCH.md "Valid forms", first row of the sc1
-// table (no agent fences: an earlier form with release/acquire fences was slower than the reduce
-// launch it replaced).  A column tile's partial lines are read once per launch, by its last arriver.
+// stores its f32 partial product (an in-kernel last-arriver reduction was measured slower: the two
+// agent-scope fences it needs cost more than the separate reduce launch).
 // MT (LNMODE 0 only): 32-row tiles per workgroup sharing every weight fragment (beam decoding).
 template <int NW, int LNMODE, int EPI, int KLN, typename OutT, int MT = 1>
 __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
@@ -224,11 +211,6 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
         reinterpret_cast<float*>(p.y)[ks * p.split_stride + (int64_t)row * p.ldy + n] = tv[k];
         continue;
       }
-      if (EPI == 3) {  // published write-through for the tile's last arriver
-        __hip_atomic_store(reinterpret_cast<float*>(p.y) + ks * p.split_stride + (int64_t)row * p.ldy + n, tv[k],
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        continue;
-      }
       float v = tv[k];
       if (p.bias) v += p.bias[n];
       if (EPI >= 1) {
@@ -238,35 +220,6 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
         if (p.gelu) v = gelu_tanh_d(v);
         St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
       }
-    }
-  }
-  if constexpr (EPI == 3) {
-    static_assert(MT == 1, "last-arriver reduce: one 32-row tile per launch");
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int old = __hip_atomic_fetch_add(p.cnt + nt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = old == nsplit - 1;
-      if (old == nsplit - 1) __hip_atomic_store(p.cnt + nt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!last) return;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int o = threadIdx.x + 64 * NW * k;
-      const int r = o / 64, l = o % 64;
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-      const int n = nt * 32 + (l & 31);
-      if (row >= p.M || n >= p.N) continue;
-      const float* P = reinterpret_cast<const float*>(p.y) + (int64_t)row * p.ldy + n;
-      float v = p.bias ? p.bias[n] : 0.f;
-      for (int sp = 0; sp < nsplit; ++sp)
-        v += __hip_atomic_load(P + sp * p.split_stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      float* X = p.x + (int64_t)row * p.ldx + n;
-      const float xv = *X + v;
-      *X = xv;
-      p.xh[(int64_t)row * p.ldxh + n] = f2bf(xv);
     }
   }
 }
@@ -588,8 +541,7 @@ extern "C" int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed
   ITTS_REQUIRE(ksplit >= 1 && (K / 16) % ksplit == 0, fn, "K/16 must be a multiple of ksplit");
   ITTS_REQUIRE(ksplit == 1 || epi == 2, fn, "ksplit > 1 requires epi 2");
   ITTS_REQUIRE(epi != 2 || (lnmode == 0 && split_stride >= (int64_t)M * ldy), fn, "bad split-K partial layout");
-  DgArgs d{a,  lda,          static_cast<const u32x4_t*>(w_packed), K,       N,       M,    bias, g1, b1, g2, b2,
-           gelu, y, ldy, split_stride, nullptr, 0, nullptr, 0, nullptr};
+  DgArgs d{a, lda, static_cast<const u32x4_t*>(w_packed), K, N, M, bias, g1, b1, g2, b2, gelu, y, ldy, split_stride};
   const int tiles = (M + 31) / 32;
   hipStream_t s = itts::as_stream(stream);
 #define DG_LN(NWV, LNM, EPIV, OT)                                            \
@@ -620,27 +572,6 @@ extern "C" int itts_decode_gemm(const void* a, int64_t lda, const void* w_packed
   return itts::check_launch(fn);
 }
 
-// Split-K residual projection with the reduction in the same launch (EPI 3): x += bias + a @ W^T,
-// xh = bf16(x), for M <= 32 rows; part [ksplit][M][ldp] f32 scratch, cnt [ceil(N/32)] ints, zero
-// before the first launch and left zero by every launch.  Bit-identical to itts_decode_gemm (epi 2)
-// followed by itts_residual_reduce_ln without LayerNorm.
-extern "C" int itts_decode_gemm_reduce(const void* a, int64_t lda, const void* w_packed, int K, int N, int M,
-                                       const float* bias, float* part, int64_t ldp, int64_t split_stride, int ksplit,
-                                       float* x, int64_t ldx, void* xh, int64_t ldxh, int* cnt, void* stream) {
-  const char* fn = "itts_decode_gemm_reduce";
-  ITTS_REQUIRE(M >= 0 && M <= 32 && N > 0 && K > 0 && K % 16 == 0, fn, "bad sizes (M <= 32)");
-  if (M == 0) return 0;
-  ITTS_REQUIRE(a && w_packed && part && x && xh && cnt, fn, "null pointer");
-  ITTS_REQUIRE(ksplit >= 1 && (K / 16) % ksplit == 0, fn, "K/16 must be a multiple of ksplit");
-  ITTS_REQUIRE(ldp >= N && split_stride >= (int64_t)M * ldp, fn, "bad partial layout");
-  DgArgs d{a, lda, static_cast<const u32x4_t*>(w_packed), K, N, M, bias, nullptr, nullptr, nullptr, nullptr, 0,
-           part, ldp, split_stride, x, ldx, static_cast<uint16_t*>(xh), ldxh, cnt};
-  hipStream_t s = itts::as_stream(stream);
-  hipLaunchKernelGGL((decode_gemm_kernel<8, 0, 3, 256, float, 1>), dim3((N + 31) / 32, ksplit), dim3(512),
-                     (size_t)8 * 16 * 64 * sizeof(float), s, d);
-  return itts::check_launch(fn);
-}
-
 // 16-column tiles, store epilogue: y = act(a @ W^T + bias) as out_dtype (act = gelu_tanh if gelu);
 // weights from pack_skinny16; a: bf16 rows padded to whole 32-row tiles.
 extern "C" int itts_decode_gemm16(const void* a, int64_t lda, const void* w_packed16, int K, int N, int M,
@@ -651,7 +582,7 @@ extern "C" int itts_decode_gemm16(const void* a, int64_t lda, const void* w_pack
   ITTS_REQUIRE(a && w_packed16 && y, fn, "null pointer");
   ITTS_REQUIRE(lda % 8 == 0 && (reinterpret_cast<uintptr_t>(a) & 15) == 0, fn, "A rows must be 16-B aligned");
   DgArgs d{a, lda, static_cast<const u32x4_t*>(w_packed16), K, N, M, bias, nullptr, nullptr, nullptr, nullptr,
-           gelu, y, ldy, 0, nullptr, 0, nullptr, 0, nullptr};
+           gelu, y, ldy, 0};
   const int tiles = (M + 31) / 32;
   hipStream_t s = itts::as_stream(stream);
   if (out_dtype == ITTS_BF16) launch_dg16<8, uint16_t>(d, tiles, s);

@@ -37,8 +37,12 @@ extern "C" int itts_gpt_decode_state_bytes(const ItTsGptWeights* w, int rows, in
   return 0;
 }
 
-extern "C" int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecodeState* st, const ItTsSampling* smp,
-                                    void* stream) {
+namespace {
+// one decode step without the step-counter advance; step k of a multi-step call reads key
+// kv_base + tstate[0] + k and writes code column tstate[0] + 1 + k (so ONE advance by n follows n
+// steps: the advance kernel is a whole dependent launch per step otherwise)
+int decode_step_impl(const ItTsGptWeights* w, const ItTsGptDecodeState* st, const ItTsSampling* smp, int k,
+                     void* stream) {
   const char* fn = "itts_gpt_decode_step";
   ITTS_REQUIRE(w && st && smp && w->layers, fn, "null pointer");
   const int L = w->n_layer, D = w->d_model, H = w->n_head, R = st->rows;
@@ -64,11 +68,11 @@ extern "C" int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecode
     // attention (appends this step's k/v); beams read their keys through the lineage table
     if (rc == 0 && st->kv_rows)
       rc = itts_attn_decode_rows(st->qkv, 3 * D, 1, (int64_t)R * 3 * D, nullptr, kc, vc, cache_bs, cache_hs,
-                                 st->max_kv, st->pad, st->kv_base, st->tstate, st->o, D, R, H, ITTS_BF16, ITTS_BF16,
+                                 st->max_kv, st->pad, st->kv_base + k, st->tstate, st->o, D, R, H, ITTS_BF16, ITTS_BF16,
                                  st->kv_rows, st->ld_rows, stream);
     else if (rc == 0)
       rc = itts_attn_decode(st->qkv, 3 * D, 1, (int64_t)R * 3 * D, nullptr, kc, vc, cache_bs, cache_hs, st->max_kv,
-                            st->pad, st->kv_base, st->tstate, st->o, D, R, H, ITTS_BF16, ITTS_BF16, stream);
+                            st->pad, st->kv_base + k, st->tstate, st->o, D, R, H, ITTS_BF16, ITTS_BF16, stream);
     // attn.c_proj: x += o W_o + b_o, x^ = bf16(x)
     if (rc == 0)
       rc = itts_decode_gemm16x(st->o, D, ly.o_w16, D, D, R, ly.o_c, nullptr, eps, 0, 1, st->x, D, ITTS_F32, st->xh, D,
@@ -92,14 +96,33 @@ extern "C" int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecode
   if (rc) return rc;
   if (smp->mode == 0) {
     rc = itts_sample_embed(st->logits, w->logits_pitch, w->n_mel_codes, st->seen, st->done, st->codes, st->max_new,
-                           st->tstate, 1, smp->min_new, w->stop_mel, smp->rep_penalty, w->mel_emb, w->mel_pos, 2, D,
+                           st->tstate, 1 + k, smp->min_new, w->stop_mel, smp->rep_penalty, w->mel_emb, w->mel_pos, 2, D,
                            nullptr, nullptr, st->x, st->xh, ITTS_BF16, R, st->forced, stream);
   } else if (smp->mode == 1) {
     rc = itts_sample_topk_embed(st->logits, w->logits_pitch, w->n_mel_codes, st->seen, st->done, st->codes,
-                                st->max_new, st->tstate, 1, smp->min_new, w->stop_mel, smp->rep_penalty,
+                                st->max_new, st->tstate, 1 + k, smp->min_new, w->stop_mel, smp->rep_penalty,
                                 smp->temperature, smp->top_k, smp->top_p, w->mel_emb, w->mel_pos, 2, D, nullptr,
                                 nullptr, st->x, st->xh, ITTS_BF16, R, st->forced, stream);
   }
+  return rc;
+}
+}  // namespace
+
+extern "C" int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecodeState* st, const ItTsSampling* smp,
+                                    void* stream) {
+  int rc = decode_step_impl(w, st, smp, 0, stream);
   if (rc == 0 && smp->mode != 2) rc = itts_step_advance(st->tstate, 1, stream);
+  return rc;
+}
+
+extern "C" int itts_gpt_decode_steps(const ItTsGptWeights* w, const ItTsGptDecodeState* st, const ItTsSampling* smp,
+                                     int nsteps, void* stream) {
+  const char* fn = "itts_gpt_decode_steps";
+  ITTS_REQUIRE(w && st && smp, fn, "null pointer");
+  ITTS_REQUIRE(nsteps >= 1 && nsteps <= 64, fn, "nsteps must be in [1, 64]");
+  ITTS_REQUIRE(nsteps == 1 || smp->mode != 2, fn, "beam decoding (mode 2) runs one step per call");
+  int rc = 0;
+  for (int k = 0; k < nsteps && rc == 0; ++k) rc = decode_step_impl(w, st, smp, k, stream);
+  if (rc == 0 && smp->mode != 2) rc = itts_step_advance(st->tstate, nsteps, stream);
   return rc;
 }

@@ -71,8 +71,6 @@ SIGNATURES = {
     "itts_step_advance": (_c_i, [_vp, _c_i, _vp]),
     "itts_decode_gemm": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _vp,
                                 _c_i64, _c_i, _c_i64, _c_i, _vp]),
-    "itts_decode_gemm_reduce": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _c_i64, _c_i64, _c_i, _vp,
-                                       _c_i64, _vp, _c_i64, _vp, _vp]),
     "itts_gpt_decode_state_bytes": (_c_i, [_vp, _c_i, _c_i, _c_i, _vp]),
     "itts_gpt_decode_step": (_c_i, [_vp, _vp, _vp, _vp]),
     "itts_gpt_decode_steps": (_c_i, [_vp, _vp, _vp, _c_i, _vp]),

@@ -356,10 +356,11 @@ class HipGPT:
             0 if kv_rows is None else kv_rows.stride(0), p(st["seen"]), p(st["done"]), p(st["codes"]),
             p(st.get("forced")))
 
-    def _decode_step_c(self, st, min_new, penalty):
+    def _decode_step_c(self, st, min_new, penalty, nsteps=1):
         """bf16 product decode step as ONE C-ABI call (itts_gpt_decode_step, gpt_step.hip): the launches
         of _decode_step_fold, mel_head, token selection, step advance.  Bit-identical to
-        _decode_step_fold (tests/test_gpu_cstep.py)."""
+        _decode_step_fold (tests/test_gpu_cstep.py).  nsteps > 1 (not beams): that many steps in one
+        call with one step-counter advance (itts_gpt_decode_steps)."""
         beams = "kv_rows" in st
         smp = st.get("sampling")
         if beams:
@@ -370,6 +371,11 @@ class HipGPT:
             mode = _hip.Sampling(1, int(min_new), float(penalty), float(smp[0]), int(smp[1]), float(smp[2]))
         cst = self._c_state(st)
         stream = _hip.stream_ptr()
+        if nsteps > 1:
+            assert not beams
+            _hip.check(self.lib.itts_gpt_decode_steps(ctypes.byref(self._cweights), ctypes.byref(cst),
+                                                      ctypes.byref(mode), int(nsteps), stream), "itts_gpt_decode_steps")
+            return
         _hip.check(self.lib.itts_gpt_decode_step(ctypes.byref(self._cweights), ctypes.byref(cst), ctypes.byref(mode),
                                                  stream), "itts_gpt_decode_step")
         if beams:
@@ -672,12 +678,12 @@ class HipGPT:
             fc[:, : forced.shape[1]] = forced.to(self.dev, torch.int32)
             if st.get("forced") is None:
                 st["forced"] = fc
-                ln["graph"] = None
+                ln["graph"] = ln["multi"] = None  # both graphs hold the forced-codes pointer
             else:
                 st["forced"].copy_(fc)
         elif st.get("forced") is not None:
             st["forced"] = None
-            ln["graph"] = None
+            ln["graph"] = ln["multi"] = None
         # ---- prefill over [B, s+1] rows ----
         M = B * (s + 1)
         x = emb.reshape(M, self.D).contiguous()
@@ -717,8 +723,11 @@ class HipGPT:
             saved = {k: st[k].clone() for k in keys}
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                for _ in range(n):
-                    self._decode_step(st, min_new, penalty)
+                if self.cstep and "kv_rows" not in st:  # n steps, one counter advance
+                    self._decode_step_c(st, min_new, penalty, nsteps=n)
+                else:
+                    for _ in range(n):
+                        self._decode_step(st, min_new, penalty)
             for k, v in saved.items():
                 st[k].copy_(v)
             mg = ln["multi"] = (g, (n, gkey))

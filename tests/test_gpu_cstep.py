@@ -80,3 +80,24 @@ def test_step_beams_same_hypotheses(do_sample):
     c0, _ = _run(eng, False, conds, text, 32, **kw)
     c1, _ = _run(eng, True, conds, text, 32, **kw)
     assert torch.equal(c0, c1)
+
+
+@pytest.mark.parametrize("sample", [False, True])
+def test_multi_step_call_equals_single_steps(sample, monkeypatch):
+    """itts_gpt_decode_steps (4 steps per captured graph, one counter advance) vs one-step graph
+    replays of itts_gpt_decode_step: identical ids / draws over 50 steps (several 4-step replays,
+    the done-check boundaries, and the single-step tail)."""
+    from indextts.gpt.engine import HipGPT
+    eng = _engine("full")
+    conds, text = _inputs(eng, 32, 16, 96, 3)
+    kw = dict(min_new_tokens=50, repetition_penalty=10.0)
+    if sample:
+        kw.update(do_sample=True, top_k=30, top_p=0.8, seed=77)
+    monkeypatch.setattr(HipGPT, "GRAPH_STEPS", 1)
+    c1 = eng.generate(conds, text, 50, **kw).cpu()
+    monkeypatch.setattr(HipGPT, "GRAPH_STEPS", 4)
+    for ln in eng._lanes.values():
+        if isinstance(ln, dict):
+            ln["multi"] = None
+    c4 = eng.generate(conds, text, 50, **kw).cpu()
+    assert torch.equal(c1, c4)
