@@ -34,7 +34,8 @@ const char* itts_last_error(void);
 int itts_abi_version(void);
 const char* itts_build_target(void); /* "gfx950" */
 /* sizeof of the ABI structs below (0 ItTsGptLayerW, 1 ItTsGptWeights, 2 ItTsGptDecodeState,
- * 3 ItTsSampling, 4 ItTsConv, 5 ItTsAct, 6 ItTsAmpLayer, 7 ItTsBigvganStage, 8 ItTsBigvganWeights),
+ * 3 ItTsSampling, 4 ItTsConv, 5 ItTsAct, 6 ItTsAmpLayer, 7 ItTsBigvganStage, 8 ItTsBigvganWeights,
+ * 9 ItTsGptSeqLayerW, 10 ItTsGptSeqWeights),
  * -1 otherwise: lets a binding check its struct layouts. */
 int64_t itts_struct_size(int which);
 
@@ -335,6 +336,43 @@ typedef struct ItTsSampling {
  * forced: caller's choice).  A host without Python allocates these and fills ItTsGptDecodeState. */
 #define ITTS_GPT_STATE_NBUF 14
 int itts_gpt_decode_state_bytes(const ItTsGptWeights* w, int rows, int max_kv, int max_new, int64_t* bytes);
+/* ---- full-sequence passes (prefill, teacher-forced latent pass) ---------------------------------- */
+/* One GPT-2 block's weights for the sequence GEMMs: bf16 mode = the implicit-GEMM packing of W^T [N][K]
+ * (itts_igemm_pack_dims, 1 tap), f32 mode = f32 W^T [N][K] (HF Conv1D [in][out] transposed). */
+typedef struct ItTsGptSeqLayerW {
+  const void *qkv_w, *o_w, *fc_w, *proj_w;
+  const float *qkv_b, *o_b, *fc_b, *proj_b;
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+} ItTsGptSeqLayerW;
+typedef struct ItTsGptSeqWeights {
+  int n_layer, d_model, n_head, dtype; /* dtype ITTS_BF16 (MFMA product mode) or ITTS_F32 (exact f32) */
+  const ItTsGptSeqLayerW* layers;
+  const float *ln_f_g, *ln_f_b, *final_g, *final_b;
+  const float* head_w_f32;             /* f32 mode: mel_head W [n_mel_codes][d_model] (prefill) */
+} ItTsGptSeqWeights;
+/* Workspace bytes of itts_gpt_forward_rows / itts_gpt_prefill for M packed rows. */
+int64_t itts_gpt_forward_rows_workspace_bytes(const ItTsGptSeqWeights* w, int64_t M);
+/* Every GPT-2 block over nseq packed sequences (rows seq_start[i] .. + seq_len[i] of x [M][D] f32, in
+ * place; keys before seq_pad[i] masked, Q2; causal), writing K/V into the decode cache when cache_k is
+ * non-NULL (layer l at cache + l * cache_layer_stride elements, [seq][head][pos][64]); then
+ * out[i] = final_norm(ln_f(x[out_idx[i]])) for n_out rows (Q5).  The teacher-forced latent pass of
+ * UnifiedVoice.forward(return_latent=True) (gpt/model.py:521-578, get_logits :462-477) and the prefill
+ * forward of generate; HF modeling_gpt2.py:246-306 per block. */
+int itts_gpt_forward_rows(const ItTsGptSeqWeights* w, float* x, int64_t M, const int32_t* seq_start,
+                          const int32_t* seq_len, const int32_t* seq_pad, int nseq, int max_len, void* cache_k,
+                          void* cache_v, int64_t cache_bs, int64_t cache_hs, int64_t cache_layer_stride,
+                          int cache_dtype, const int32_t* out_idx, int n_out, void* out, int out_dtype,
+                          void* workspace, void* stream);
+/* The first iteration of generate for every row of a decode state: emb [rows][s+1][D] f32 (the
+ * prepare_gpt_inputs block + the start-mel embedding; consumed) through the layers into the state's
+ * KV cache (seq_start[b] = b*(s+1), seq_len[b] = s+1, padding st->pad), final_norm(ln_f(.)) of each
+ * row's last position (last_idx[b]) -> mel_head -> the first token (ItTsSampling modes 0 / 1, code
+ * column 0) and the next embedding; mode 2 stops at the logits (beam search).  Then
+ * itts_gpt_decode_step(s) continue.  gpt/model.py:85-192 (prefill branch), :655-708. */
+int itts_gpt_prefill(const ItTsGptSeqWeights* ws, const ItTsGptWeights* w, const ItTsGptDecodeState* st, float* emb,
+                     int s, const int32_t* seq_start, const int32_t* seq_len, const int32_t* last_idx,
+                     const ItTsSampling* sampling, void* workspace, void* stream);
+
 /* One whole KV-cached decode step (one HF generate iteration of inference_speech, gpt/model.py:655-708),
  * per layer: c_attn with ln_1 folded (itts_decode_gemm16x) -> itts_attn_decode[_rows] -> attn.c_proj
  * (itts_decode_gemm16x residual) -> c_fc with ln_2 folded + gelu -> mlp.c_proj split-K 8

@@ -57,6 +57,9 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 #ifndef ITTS_ATTN_WPS
 #define ITTS_ATTN_WPS 1
 #endif
+#ifndef ITTS_ATTN_GUARD
+#define ITTS_ATTN_GUARD 1
+#endif
 #ifndef ITTS_ATTN_PROJ_WPS  // fused c_proj: 256 VGPRs without spills at 1; 2 spills 96 VGPRs
 #define ITTS_ATTN_PROJ_WPS 1
 #endif
@@ -121,10 +124,16 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
   // (2) this round's cached K rows, then its V rows (the scores need only K).  Every lane loads a valid
   // row (key index clamped into the cache), so the loads are unconditional and retire in order; rows
   // past the round's keys are never used.
-  u32x4_t kr[KB][RW], vr[KB][RW];
+  u32x4_t kr[KB][RW] = {}, vr[KB][RW] = {};
   auto kv_load = [&](u32x4_t (&dst)[KB][RW], const TC* base, int j0) {
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
+#if ITTS_ATTN_GUARD
+      // slots whose whole 8-row block lies past the keys are not loaded (workgroup-uniform test): a
+      // short sequence (long-form chunks, early steps) does not pay KB rows per lane; such slots are
+      // never read (keys j >= nk - 1 take this step's k / v from LDS)
+      if (j0 + NG * u >= nk - 1) continue;
+#endif
       const int j = min(j0 + NG * u + g, max(nk - 2, 0));
 #pragma unroll
       for (int w = 0; w < RW; ++w) {

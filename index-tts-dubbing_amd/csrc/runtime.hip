@@ -25,7 +25,7 @@ int check_launch(const char* fn) {
 
 extern "C" const char* itts_last_error(void) { return itts::g_last_error.c_str(); }
 
-extern "C" int itts_abi_version(void) { return 1; }
+extern "C" int itts_abi_version(void) { return 2; }  // 2: sequence passes, multi-step decode
 
 // Which gfx target this code object was built for (sanity check from the host).
 extern "C" const char* itts_build_target(void) { return "gfx950"; }
@@ -43,6 +43,8 @@ extern "C" int64_t itts_struct_size(int which) {
     case 6: return sizeof(ItTsAmpLayer);
     case 7: return sizeof(ItTsBigvganStage);
     case 8: return sizeof(ItTsBigvganWeights);
+    case 9: return sizeof(ItTsGptSeqLayerW);
+    case 10: return sizeof(ItTsGptSeqWeights);
     default: return -1;
   }
 }

@@ -71,6 +71,10 @@ SIGNATURES = {
     "itts_step_advance": (_c_i, [_vp, _c_i, _vp]),
     "itts_decode_gemm": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i, _c_i, _vp, _vp, _vp, _vp, _vp, _c_i, _c_i, _c_i, _vp,
                                 _c_i64, _c_i, _c_i64, _c_i, _vp]),
+    "itts_gpt_forward_rows_workspace_bytes": (_c_i64, [_vp, _c_i64]),
+    "itts_gpt_forward_rows": (_c_i, [_vp, _vp, _c_i64, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _c_i64, _c_i64, _c_i64,
+                                     _c_i, _vp, _c_i, _vp, _c_i, _vp, _vp]),
+    "itts_gpt_prefill": (_c_i, [_vp, _vp, _vp, _vp, _c_i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "itts_gpt_decode_state_bytes": (_c_i, [_vp, _c_i, _c_i, _c_i, _vp]),
     "itts_gpt_decode_step": (_c_i, [_vp, _vp, _vp, _vp]),
     "itts_gpt_decode_steps": (_c_i, [_vp, _vp, _vp, _c_i, _vp]),
@@ -99,6 +103,17 @@ class GptDecodeState(ctypes.Structure):
         [(n, _vp) for n in ("x", "xh", "qkv", "o", "f", "part", "logits", "k_cache", "v_cache", "pad", "tstate",
                             "kv_rows")] + \
         [("ld_rows", _c_i64)] + [(n, _vp) for n in ("seen", "done", "codes", "forced")]
+
+
+class GptSeqLayerW(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("qkv_w", "o_w", "fc_w", "proj_w", "qkv_b", "o_b", "fc_b", "proj_b", "ln1_g",
+                                   "ln1_b", "ln2_g", "ln2_b")]
+
+
+class GptSeqWeights(ctypes.Structure):
+    _fields_ = [("n_layer", _c_i), ("d_model", _c_i), ("n_head", _c_i), ("dtype", _c_i),
+                ("layers", ctypes.POINTER(GptSeqLayerW))] + \
+        [(n, _vp) for n in ("ln_f_g", "ln_f_b", "final_g", "final_b", "head_w_f32")]
 
 
 class Sampling(ctypes.Structure):

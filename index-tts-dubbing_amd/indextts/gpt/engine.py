@@ -243,7 +243,70 @@ class HipGPT:
         return torch.bfloat16 if self.mode == "bf16" else torch.float32
 
     # ---------------- full-sequence forward (prefill + latent pass) ----------------
-    def _forward_rows(self, x, seq_start, seq_len, seq_pad, max_len, cache=None):
+    # the sequence passes as ONE C-ABI call each (itts_gpt_forward_rows / itts_gpt_prefill, gpt_seq.hip:
+    # the launch sequence of _forward_rows_py in C++, so a non-Python host can run prefill, decode and
+    # the latent pass through the ABI alone); ITTS_CSEQ=0: the Python launch sequence (test reference)
+    cseq = os.environ.get("ITTS_CSEQ", "1") != "0"
+
+    def _c_seq_weights(self):
+        """ItTsGptSeqWeights (include/itts_hip.h) over this engine's sequence-GEMM weights."""
+        if getattr(self, "_cseqw", None) is None:
+            L = len(self.layers)
+            arr = (_hip.GptSeqLayerW * L)()
+            key = "f32" if self.mode == "f32" else "ig"
+            for i, ly in enumerate(self.layers):
+                arr[i] = _hip.GptSeqLayerW(*[ly.w[n][key].data_ptr() for n in ("qkv", "o", "fc", "proj")],
+                                           *[ly.b[n].data_ptr() for n in ("qkv", "o", "fc", "proj")],
+                                           ly.ln1[0].data_ptr(), ly.ln1[1].data_ptr(), ly.ln2[0].data_ptr(),
+                                           ly.ln2[1].data_ptr())
+            w = _hip.GptSeqWeights(L, self.D, self.H, _hip.F32 if self.mode == "f32" else _hip.BF16, arr,
+                                   self.ln_f[0].data_ptr(), self.ln_f[1].data_ptr(), self.final_norm[0].data_ptr(),
+                                   self.final_norm[1].data_ptr(),
+                                   self.head_w["f32"].data_ptr() if self.mode == "f32" else None)
+            w._layers = arr
+            self._cseqw = w
+        return self._cseqw
+
+    def _c_head_weights(self):
+        """ItTsGptWeights for the prefill's head + sampler (the decode structs in fold mode; f32 mode has
+        no packed decode layers, so a struct without them)."""
+        if self.fold:
+            return self._cweights
+        if getattr(self, "_cheadw", None) is None:
+            self._cheadw = _hip.GptWeights(self.L, self.D, self.H, self.V, self.Vp, self.start_mel, self.stop_mel, None,
+                                           self.ln_f[0].data_ptr(), self.ln_f[1].data_ptr(),
+                                           self.final_norm[0].data_ptr(), self.final_norm[1].data_ptr(),
+                                           self.head_w["sk"].data_ptr() if "sk" in self.head_w else None,
+                                           self.head_b.data_ptr(), self.mel_emb.data_ptr(), self.mel_pos.data_ptr())
+        return self._cheadw
+
+    def _seq_workspace(self, M):
+        n = int(self.lib.itts_gpt_forward_rows_workspace_bytes(ctypes.byref(self._c_seq_weights()), int(M)))
+        return torch.empty(max(n, 1), dtype=torch.uint8, device=self.dev)
+
+    def _forward_rows(self, x, seq_start, seq_len, seq_pad, max_len, cache=None, out_idx=None, out=None):
+        """x [M, D] f32 (in place) through all layers (+ out[i] = final_norm(ln_f(x[out_idx[i]])))."""
+        if not self.cseq:
+            self._forward_rows_py(x, seq_start, seq_len, seq_pad, max_len, cache)
+            if out is not None:
+                self._ln(x, out.view(-1, self.D), self.ln_f, self.final_norm, idx=out_idx, M=out_idx.numel())
+            return x
+        M, D = x.shape
+        ck = cv = None
+        cbs = chs = cls = 0
+        cdt = _hip.dtype_code(x) if self.mode == "f32" else _hip.BF16
+        if cache is not None:
+            ck, cv = cache
+            cbs, chs, cls, cdt = ck.stride(1), ck.stride(2), ck.stride(0), _hip.dtype_code(ck)
+        ws = self._seq_workspace(M)
+        _hip.check(self.lib.itts_gpt_forward_rows(
+            ctypes.byref(self._c_seq_weights()), x.data_ptr(), M, seq_start.data_ptr(), seq_len.data_ptr(),
+            _hip.ptr(seq_pad), seq_start.numel(), int(max_len), _hip.ptr(ck), _hip.ptr(cv), cbs, chs, cls, cdt,
+            _hip.ptr(out_idx), 0 if out is None else int(out_idx.numel()), _hip.ptr(out),
+            _hip.dtype_code(out) if out is not None else 0, ws.data_ptr(), _hip.stream_ptr()), "itts_gpt_forward_rows")
+        return x
+
+    def _forward_rows_py(self, x, seq_start, seq_len, seq_pad, max_len, cache=None):
         """x [M, D] f32 (modified in place) through all layers; returns x (pre ln_f)."""
         M, D = x.shape
         ad = self.act_dtype
@@ -689,14 +752,30 @@ class HipGPT:
         x = emb.reshape(M, self.D).contiguous()
         starts = torch.arange(B, dtype=torch.int32, device=self.dev) * (s + 1)
         lens = torch.full((B,), s + 1, dtype=torch.int32, device=self.dev)
-        self._forward_rows(x, starts, lens, pad, s + 1, cache=(st["kc"], st["vc"]))
         last = (starts + s).contiguous()
+        if self.cseq and (self.fold or self.mode == "f32") and "kv_rows" not in st:
+            # one C-ABI call: layers -> KV cache, head, first token + next embedding (itts_gpt_prefill)
+            st["s"] = s
+            smp = st.get("sampling")
+            mode = _hip.Sampling(0, int(min_new), float(penalty), 1.0, 0, 1.0) if smp is None else \
+                _hip.Sampling(1, int(min_new), float(penalty), float(smp[0]), int(smp[1]), float(smp[2]))
+            ws = self._seq_workspace(M)
+            _hip.check(self.lib.itts_gpt_prefill(
+                ctypes.byref(self._c_seq_weights()), ctypes.byref(self._c_head_weights()),
+                ctypes.byref(self._c_state(st)), x.data_ptr(), s, starts.data_ptr(), lens.data_ptr(), last.data_ptr(),
+                ctypes.byref(mode), ws.data_ptr(), _hip.stream_ptr()), "itts_gpt_prefill")
+            self._after_prefill(ln, st, min_new, penalty, use_graph, gkey)
+            return
+        self._forward_rows(x, starts, lens, pad, s + 1, cache=(st["kc"], st["vc"]))
         self._ln(x, st["h"], self.ln_f, self.final_norm, idx=last, M=B)
         if self.mode == "f32":
             self._gemm(st["h"][:B], self.head_w, st["logits"], bias=self.head_b)
         else:
             self._dgw(st["h"], self.head_w, B, self.head_b, st["logits"])
         self._sample(st, 0, min_new, penalty)
+        self._after_prefill(ln, st, min_new, penalty, use_graph, gkey)
+
+    def _after_prefill(self, ln, st, min_new, penalty, use_graph, gkey):
         if self.logits_trace is not None:  # the prefill's logits (before the capture's warm-up step)
             self.logits_trace.append(st["logits"][:, : self.V].clone())
         ln["graph_ok"] = False
@@ -966,15 +1045,13 @@ class HipGPT:
         x[up(mel_dst)] = self.mel_emb[up(mel_tok)] + self.mel_pos[up(mel_pos)]
         s_t = torch.from_numpy(starts.astype(np.int32)).to(dev)
         l_t = torch.tensor(lens, dtype=torch.int32, device=dev)
-        self._forward_rows(x, s_t, l_t, None, max(lens))
         Tmax = max(n)
         idx = np.zeros((B, Tmax), dtype=np.int32)
         for b in range(B):  # latent rows: the first n of the mel block (start token .. code n-2), :-2 of
             first = int(starts[b]) + ncond + int(lt[b]) + 2  # gpt/model.py:575-578
             idx[b, : n[b]] = np.arange(first, first + n[b])
         out = torch.empty(B, Tmax, self.D, dtype=self.act_dtype, device=self.dev)
-        self._ln(x, out.view(B * Tmax, self.D), self.ln_f, self.final_norm,
-                 idx=torch.from_numpy(idx).to(dev).view(-1), M=B * Tmax)
+        self._forward_rows(x, s_t, l_t, None, max(lens), out_idx=torch.from_numpy(idx).to(dev).view(-1), out=out)
         return out, torch.tensor(n, dtype=torch.int32)
 
 

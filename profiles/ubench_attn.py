@@ -5,7 +5,7 @@ import torch
 from indextts import _hip
 from ubench_decode import graph_time, lib, pack_skinny
 D, H, Smax, NKV = 1024, 16, 600, 6
-for B, S in ((32, 283), (64, 142), (128, 71), (32, 142)):
+for B, S in ((32, 283), (64, 142), (128, 71), (32, 142), (32, 90), (128, 300), (96, 283)):
     kcs = [torch.randn(B, H, Smax, 64, device="cuda").to(torch.bfloat16) for _ in range(NKV)]
     vcs = [torch.randn(B, H, Smax, 64, device="cuda").to(torch.bfloat16) for _ in range(NKV)]
     qkv = torch.randn(2 * B * 3 * D, device="cuda")

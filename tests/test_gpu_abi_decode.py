@@ -126,3 +126,156 @@ def test_decode_step_through_the_abi_only():
     chosen = codes.view(torch.int32).view(R, T).cpu()[:, 1:T].long()  # argmax recorded at col j + 1
     ok = (chosen == sel.argmax(-1)) | (margin <= 0.1)
     assert bool(ok.all()), (chosen, ref.argmax(-1))
+
+
+@pytest.mark.parametrize("size", ["tiny", "full"])
+def test_prefill_decode_latent_through_the_abi_only(size):
+    """The whole GPT side of one infer() through the header's entry points alone -- itts_gpt_prefill
+    (prompt block -> KV cache, head, first token), itts_gpt_decode_steps / itts_gpt_decode_step (the
+    loop), itts_gpt_forward_rows (teacher-forced latent pass, gpt/model.py:521-578) -- over weights the
+    test packs itself and state sized by itts_gpt_decode_state_bytes, on a left-padded batch; codes and
+    latents bit-identical to HipGPT's Python launch sequence (ITTS_CSEQ=0 path)."""
+    from indextts import _hip
+    from indextts.gpt.engine import HipGPT, fold_ln_weights, pack_skinny
+    from indextts.utils.config import default_config_path, load_config, tiny_config
+    from indextts.utils.synthetic import gpt_state_dict
+    from indextts.vocoder.bigvgan import pack_taps
+
+    lib = _hip.load()
+    cfg = (tiny_config() if size == "tiny" else load_config(default_config_path())).gpt
+    sd = gpt_state_dict(cfg, 0, 0.08)
+    dev = "cuda"
+    D, H, L, V = int(cfg.model_dim), int(cfg.heads), int(cfg.layers), int(cfg.number_mel_codes)
+    Vp = (V + 15) // 16 * 16
+    start, stop = int(cfg.start_mel_token), int(cfg.stop_mel_token)
+    B, N = 4, 40
+    g = torch.Generator().manual_seed(5)
+    conds = torch.randn(B, 32, D, generator=g).cuda()
+    text = torch.randint(2, 6000, (B, 12), generator=g)
+    text[0, :5] = 1  # left-padded rows (stop id stripped, Q3)
+    text[2, :2] = 1
+    text = text.cuda()
+
+    # ---- reference: HipGPT with the Python launch sequences
+    eng = HipGPT(sd, cfg, dev, dtype="bf16")
+    eng.cseq = False
+    want = eng.generate(conds, text, N, min_new_tokens=N, repetition_penalty=10.0).cpu()
+    texts = [t[t != 1] for t in text]
+    lat_want, lat_n = eng.latent(conds, texts, [c for c in want])
+    emb, pad, s = eng.prepare_inputs(conds, text)  # host-side table lookups (prepare_gpt_inputs)
+    torch.cuda.synchronize()
+    del eng
+
+    # ---- ABI only
+    keep = []
+
+    def dev32(v):
+        t = _t(v).float().contiguous().to(dev)
+        keep.append(t)
+        return t.data_ptr()
+
+    def lnp(i, n):
+        return sd[f"gpt.h.{i}.ln_{n}.weight"], sd[f"gpt.h.{i}.ln_{n}.bias"]
+
+    layers = (_hip.GptLayerW * L)()
+    seq_layers = (_hip.GptSeqLayerW * L)()
+    for i in range(L):
+        p = f"gpt.h.{i}."
+        qkv = fold_ln_weights(sd[p + "attn.c_attn.weight"], sd[p + "attn.c_attn.bias"], lnp(i, 1), dev)
+        o = fold_ln_weights(sd[p + "attn.c_proj.weight"], sd[p + "attn.c_proj.bias"], None, dev)
+        fc = fold_ln_weights(sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"], lnp(i, 2), dev)
+        proj = pack_skinny(_t(sd[p + "mlp.c_proj.weight"]).float().t().contiguous()).to(dev)
+        keep.extend([qkv, o, fc, proj])
+        layers[i] = _hip.GptLayerW(qkv["w16"].data_ptr(), qkv["u"].data_ptr(), qkv["c"].data_ptr(),
+                                   o["w16"].data_ptr(), o["c"].data_ptr(), fc["w16"].data_ptr(), fc["u"].data_ptr(),
+                                   fc["c"].data_ptr(), proj.data_ptr(), dev32(sd[p + "mlp.c_proj.bias"]))
+        ig = []
+        for k in ("attn.c_attn", "attn.c_proj", "mlp.c_fc", "mlp.c_proj"):
+            wt = _t(sd[p + k + ".weight"]).float().t().contiguous()  # HF Conv1D [in, out] -> [out, in]
+            t = pack_taps([wt], wt.shape[1], wt.shape[0]).to(dev)
+            keep.append(t)
+            ig.append(t.data_ptr())
+        seq_layers[i] = _hip.GptSeqLayerW(*ig, *[dev32(sd[p + k + ".bias"]) for k in
+                                                 ("attn.c_attn", "attn.c_proj", "mlp.c_fc", "mlp.c_proj")],
+                                          dev32(lnp(i, 1)[0]), dev32(lnp(i, 1)[1]), dev32(lnp(i, 2)[0]),
+                                          dev32(lnp(i, 2)[1]))
+    head = pack_skinny(_t(sd["mel_head.weight"]).float().contiguous()).to(dev)
+    keep.append(head)
+    lnf = (dev32(sd["gpt.ln_f.weight"]), dev32(sd["gpt.ln_f.bias"]), dev32(sd["final_norm.weight"]),
+           dev32(sd["final_norm.bias"]))
+    w = _hip.GptWeights(L, D, H, V, Vp, start, stop, layers, *lnf, head.data_ptr(), dev32(sd["mel_head.bias"]),
+                        dev32(sd["mel_embedding.weight"]), dev32(sd["mel_pos_embedding.emb.weight"]))
+    ws = _hip.GptSeqWeights(L, D, H, _hip.BF16, seq_layers, *lnf, None)
+
+    max_kv = s + 1 + N + 8
+    sizes = (ctypes.c_int64 * _hip.GPT_STATE_NBUF)()
+    assert lib.itts_gpt_decode_state_bytes(ctypes.byref(w), B, max_kv, N, sizes) == 0
+    buf = [torch.zeros(int(n), dtype=torch.uint8, device=dev) for n in sizes]
+    x, xh, qkv, o, f, part, logits, kc, vc, padb, tst, seen, done, codes = buf
+    padb.view(torch.int32).copy_(pad)
+    seen.view(B, Vp)[:, 1] = 1  # the prompt's fake ids 1 and 8192 count for the repetition penalty (Q4)
+    seen.view(B, Vp)[:, start] = 1
+    codes.view(torch.int32).fill_(stop)
+    st = _hip.GptDecodeState(B, max_kv, s + 1, N, x.data_ptr(), xh.data_ptr(), qkv.data_ptr(), o.data_ptr(),
+                             f.data_ptr(), part.data_ptr(), logits.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                             padb.data_ptr(), tst.data_ptr(), None, 0, seen.data_ptr(), done.data_ptr(),
+                             codes.data_ptr(), None)
+    smp = _hip.Sampling(0, N, 10.0, 1.0, 0, 1.0)
+    stream = torch.cuda.current_stream().cuda_stream
+    M = B * (s + 1)
+    work = torch.empty(int(lib.itts_gpt_forward_rows_workspace_bytes(ctypes.byref(ws), M)), dtype=torch.uint8,
+                       device=dev)
+    xin = emb.reshape(M, D).contiguous()
+    starts = (torch.arange(B, dtype=torch.int32) * (s + 1)).to(dev)
+    lens = torch.full((B,), s + 1, dtype=torch.int32, device=dev)
+    last = (starts + s).contiguous()
+    _hip.check(lib.itts_gpt_prefill(ctypes.byref(ws), ctypes.byref(w), ctypes.byref(st), xin.data_ptr(), s,
+                                    starts.data_ptr(), lens.data_ptr(), last.data_ptr(), ctypes.byref(smp),
+                                    work.data_ptr(), stream), "itts_gpt_prefill")
+    done_steps = 1
+    while done_steps < N:  # 4 steps per call while they fit, then single steps
+        n = 4 if done_steps + 4 <= N else 1
+        if n > 1:
+            _hip.check(lib.itts_gpt_decode_steps(ctypes.byref(w), ctypes.byref(st), ctypes.byref(smp), n, stream),
+                       "itts_gpt_decode_steps")
+        else:
+            _hip.check(lib.itts_gpt_decode_step(ctypes.byref(w), ctypes.byref(st), ctypes.byref(smp), stream),
+                       "itts_gpt_decode_step")
+        done_steps += n
+    torch.cuda.synchronize()
+    got = codes.view(torch.int32).view(B, N).cpu().long()
+    assert torch.equal(got[:, : want.shape[1]], want), (got, want)
+
+    # teacher-forced latent pass: [conds ; text_emb + text_pos ; mel_emb + mel_pos] per row, packed
+    te, tp = _t(sd["text_embedding.weight"]).float(), _t(sd["text_pos_embedding.emb.weight"]).float()
+    me, mp = _t(sd["mel_embedding.weight"]).float(), _t(sd["mel_pos_embedding.emb.weight"]).float()
+    rows, st_l, ln_l, idx = [], [], [], []
+    off = 0
+    for b in range(B):
+        tt = torch.cat([torch.tensor([int(cfg.start_text_token)]), texts[b].cpu(), torch.tensor([int(cfg.stop_text_token)])])
+        mm = torch.cat([torch.tensor([start]), want[b], torch.tensor([stop])])
+        r = torch.cat([conds[b].cpu(), te[tt] + tp[torch.arange(tt.numel())], me[mm] + mp[torch.arange(mm.numel())]])
+        rows.append(r)
+        st_l.append(off)
+        ln_l.append(r.shape[0])
+        first = off + 32 + tt.numel()
+        idx.append(torch.arange(first, first + int(lat_n[b])))
+        off += r.shape[0]
+    xl = torch.cat(rows).to(dev).contiguous()
+    Tm = int(lat_n.max())
+    out_idx = torch.zeros(B, Tm, dtype=torch.int32)
+    for b in range(B):
+        out_idx[b, : idx[b].numel()] = idx[b].int()
+    out_idx = out_idx.to(dev).view(-1)
+    lat = torch.empty(B, Tm, D, dtype=torch.bfloat16, device=dev)
+    work = torch.empty(int(lib.itts_gpt_forward_rows_workspace_bytes(ctypes.byref(ws), xl.shape[0])),
+                       dtype=torch.uint8, device=dev)
+    s_t, l_t = torch.tensor(st_l, dtype=torch.int32, device=dev), torch.tensor(ln_l, dtype=torch.int32, device=dev)
+    _hip.check(lib.itts_gpt_forward_rows(ctypes.byref(ws), xl.data_ptr(), xl.shape[0], s_t.data_ptr(), l_t.data_ptr(),
+                                         None, B, max(ln_l), None, None, 0, 0, 0, _hip.BF16, out_idx.data_ptr(),
+                                         B * Tm, lat.data_ptr(), _hip.BF16, work.data_ptr(), stream),
+               "itts_gpt_forward_rows")
+    torch.cuda.synchronize()
+    for b in range(B):
+        n = int(lat_n[b])
+        assert torch.equal(lat[b, :n].cpu(), lat_want[b, :n].cpu()), b
