@@ -58,7 +58,7 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 #define ITTS_ATTN_WPS 1
 #endif
 #ifndef ITTS_ATTN_GUARD
-#define ITTS_ATTN_GUARD 1
+#define ITTS_ATTN_GUARD 0  // measured slower for every KB at every shape (profiles/ubench_attn_kb_r03.txt)
 #endif
 #ifndef ITTS_ATTN_PROJ_WPS  // fused c_proj: 256 VGPRs without spills at 1; 2 spills 96 VGPRs
 #define ITTS_ATTN_PROJ_WPS 1

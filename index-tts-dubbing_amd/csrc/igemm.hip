@@ -250,6 +250,259 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
   }
 }
 
+// ---- 256-row tiles staged by LDS-DMA (global_load_lds_dwordx4) ----------------------------------
+// For the wide layers (Cin >= 128 channels, Cout a multiple of 128, >= 256): the GPT latent-pass /
+// prefill GEMMs (M = thousands of rows, K 1024 / 4096, N 1024 .. 4096), conv_pre and the C = 768 /
+// 384 generator stages.  One 512-thread workgroup per 256 x TN output tile, 8 waves (WAVES_M x
+// WAVES_N) of 32x32x16 MFMAs, K steps of 32 channels of one tap.  Each step's A (256 rows) and B (TN
+// rows of the packed W^T) images land in LDS straight from global memory -- no register stage, no
+// ds_write pass -- in a ring of 4 step images with 3 steps in flight: step it+3 is issued before step
+// it's MFMAs, and a counted s_waitcnt vmcnt (2 steps may stay outstanding) + raw s_barrier retire step
+// it+1 (a __syncthreads() would drain every DMA with vmcnt(0); MI355X guide §5 "Pipelining across
+// barriers").  One 1 KiB DMA wave-instruction fills 16 rows of 64 B.
+// LDS image: 64-B rows (32 bf16 channels), 16-B slot s of row r stored at slot s ^ ((r >> 2) & 3): the
+// 16 rows of one ds_read_b128 lane group fall on 16 distinct bank quads; the DMA writes lane-linearly,
+// so each lane loads the SOURCE slot that lands at its destination (the permutation is an involution).
+// Rows outside [0, len) (zero "same" padding, ragged lengths), channels >= Cin and W rows >= co_pad
+// load from a zero line.  Epilogue: per 32-row band the wave's accumulators go through LDS as f32
+// rows, then 16-B row-contiguous reads / residual loads / stores (the scattered 2-B stores of the
+// fragment layout were the kernel's tail).
+__device__ __attribute__((aligned(256))) uint32_t g_zero_line[64];  // 256 zero bytes (module-initialised)
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int TN, int WAVES_M, int WAVES_N, int BK, int NSLOT, typename OutT>
+__global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
+  constexpr int TM = 256, ROWB = BK * 2, SPR = BK / 8, RPI = 1024 / ROWB;  // 16-B slots per row, rows per DMA
+  constexpr int D = NSLOT - 1;  // K steps in flight ahead of the one computed
+  constexpr int WM = TM / WAVES_M, WN = TN / WAVES_N, FM = WM / 32, FN = WN / 32;
+  constexpr int A_BYTES = TM * ROWB, B_BYTES = TN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INS = TM / RPI / 8, B_INS = TN / RPI / 8;  // DMA instructions per wave per K step
+  constexpr int P = A_INS + B_INS;
+  constexpr int EP = WN + 4;  // epilogue staging pitch (floats): rows r and r + 4 on other banks
+  static_assert(WAVES_M * WAVES_N == 8 && B_INS >= 1 && (BK == 32 || BK == 64) && D >= 1, "geometry");
+  static_assert(8 * 32 * EP * 4 <= NSLOT * STAGE, "epilogue staging fits the ring");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // slot permutation of a row (an involution on the row's SPR slots): 16 consecutive rows of a fragment
+  // read fall on 16 distinct bank quads
+  auto swz = [](int row) { return SPR == 4 ? (row >> 2) & 3 : (row >> 1) & 7; };
+
+  const int ntn = (p.Cout + TN - 1) / TN, ntm = (p.Tmax + TM - 1) / TM;
+  const int nblk = ntn * ntm * p.B;
+  const int pid = blockIdx.x, xcd = pid % 8, qn = nblk / 8, rn = nblk % 8;
+  const int lid = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + pid / 8;
+  const int b = lid / (ntn * ntm);
+  const int len = p.lens ? p.lens[b] : p.Tmax;
+  const int q0 = ((lid / ntn) % ntm) * TM;
+  if (q0 >= len) return;
+  const int n0 = (lid % ntn) * TN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const uint16_t* X = p.x + (int64_t)b * p.sxb;
+  const int nchunks = p.ci_pad / BK;
+  const int kiters = p.ntaps * nchunks;
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  // DMA of K step it into ring slot it % NSLOT: lane l of an instruction covers row R + l / SPR,
+  // physical slot l % SPR = logical slot (l % SPR) ^ swz(row)
+  const int lr = lane / SPR, ls = lane % SPR;
+  auto issue = [&](int it) {
+    const int j = it / nchunks, c0 = (it - j * nchunks) * BK;
+    const int toff = p.tap_off[j];
+    unsigned char* As = smem + (it % NSLOT) * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      const int R = (wave * A_INS + i) * RPI, row = R + lr;
+      const int s = ls ^ swz(row);
+      const int t = q0 + row + toff, c = c0 + 8 * s;
+      const void* src = (t >= 0 && t < len && c < p.Cin) ? static_cast<const void*>(X + (int64_t)t * p.ldx + c)
+                                                         : static_cast<const void*>(g_zero_line);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(As + R * ROWB), 16, 0, 0);
+    }
+    unsigned char* Bs = As + A_BYTES;
+    const uint16_t* Wj = p.w + (int64_t)j * p.co_pad * p.ci_pad + c0;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      const int R = (wave * B_INS + i) * RPI, row = R + lr;
+      const int s = ls ^ swz(row);
+      const int n = n0 + row;
+      const void* src = n < p.co_pad ? static_cast<const void*>(Wj + (int64_t)n * p.ci_pad + 8 * s)
+                                     : static_cast<const void*>(g_zero_line);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(Bs + R * ROWB), 16, 0, 0);
+    }
+  };
+  // retire step it+1: later steps (up to D - 1 of them) may stay in flight
+  auto retire_next = [&](int it) {
+    const int later = min(it + D, kiters - 1) - (it + 1);
+    if (later >= 2) wait_vm<2 * P>();
+    else if (later == 1) wait_vm<P>();
+    else wait_vm<0>();
+  };
+
+  f32x16_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int r32 = lane & 31, h = lane >> 5;
+  auto compute = [&](int it) {
+    const unsigned char* As = smem + (it % NSLOT) * STAGE;
+    const unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm + 32 * i + r32;
+        af[i] = *reinterpret_cast<const bf16x8_t*>(As + row * ROWB + (((2 * ks + h) ^ swz(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn + 32 * j + r32;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + row * ROWB + (((2 * ks + h) ^ swz(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  // prologue: steps 0 .. D-1 in flight, step 0 retired
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+    if (k < kiters) issue(k);
+  retire_next(-1);
+  lds_barrier();
+  for (int it = 0; it < kiters; ++it) {
+    // slot (it + D) % NSLOT was last read in step it - 1, which every wave finished before the last barrier
+    if (it + D < kiters) issue(it + D);
+    compute(it);
+    retire_next(it);
+    lds_barrier();
+  }
+
+  // ---- epilogue: per 32-row band, f32 rows through this wave's LDS staging, 16-B row accesses
+  float* stg = reinterpret_cast<float*>(smem) + wave * 32 * EP;
+  OutT* Y = reinterpret_cast<OutT*>(p.y) + (int64_t)b * p.syb;
+  const OutT* R1 = reinterpret_cast<const OutT*>(p.r1);
+  const OutT* R2 = reinterpret_cast<const OutT*>(p.r2);
+  if (R1) R1 += (int64_t)b * p.syb;
+  if (R2) R2 += (int64_t)b * p.syb;
+  float bn[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn + 32 * j + r32;
+    bn[j] = 0.f;
+    if (n < p.Cout) {
+      if (p.bias) bn[j] = p.bias[n];
+      if (p.bias_b) bn[j] += p.bias_b[(int64_t)b * p.Cout + n];
+    }
+  }
+  constexpr int V = 16 / sizeof(OutT);  // outputs per 16-B store
+  constexpr int CPR = WN / V;            // chunks per staged row
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = acc[i][j][r] + bn[j];
+        if (p.gelu) v = gelu_tanh(v);
+        stg[((r & 3) + 8 * (r >> 2) + 4 * h) * EP + 32 * j + r32] = v;
+      }
+#pragma unroll
+    for (int k = 0; k < 32 * CPR / 64; ++k) {
+      const int c = lane + 64 * k, row = c / CPR, col = (c - row * CPR) * V;
+      const int q = q0 + wm + 32 * i + row, n = n0 + wn + col;
+      float v[V];
+#pragma unroll
+      for (int e = 0; e < V; e += 4) {
+        const f32x4_t f = *reinterpret_cast<const f32x4_t*>(stg + row * EP + col + e);
+        v[e] = f[0];
+        v[e + 1] = f[1];
+        v[e + 2] = f[2];
+        v[e + 3] = f[3];
+      }
+      if (q < len && n < p.Cout) {
+        const int64_t off = (int64_t)(q * p.ymul + p.yoff) * p.ldy + n;
+        if constexpr (sizeof(OutT) == 4) {
+          if (R1) {
+            const f32x4_t a = *reinterpret_cast<const f32x4_t*>(R1 + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += a[e];
+          }
+          if (R2) {
+            const f32x4_t a = *reinterpret_cast<const f32x4_t*>(R2 + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += a[e];
+          }
+          *reinterpret_cast<f32x4_t*>(Y + off) =
+              f32x4_t{p.alpha * v[0], p.alpha * v[1], p.alpha * v[2], p.alpha * v[3]};
+        } else {
+          if (R1) {
+            const u32x4_t a = *reinterpret_cast<const u32x4_t*>(R1 + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] += __uint_as_float(a[e] << 16);
+              v[2 * e + 1] += __uint_as_float(a[e] & 0xFFFF0000u);
+            }
+          }
+          if (R2) {
+            const u32x4_t a = *reinterpret_cast<const u32x4_t*>(R2 + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] += __uint_as_float(a[e] << 16);
+              v[2 * e + 1] += __uint_as_float(a[e] & 0xFFFF0000u);
+            }
+          }
+          u32x4_t o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = pack2bf(p.alpha * v[2 * e], p.alpha * v[2 * e + 1]);
+          *reinterpret_cast<u32x4_t*>(Y + off) = o;
+        }
+      }
+    }
+  }
+}
+
+// ITTS_IGEMM_256=0 keeps the register-staged 128-row tiles for every layer (A/B measurements)
+bool igemm256_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ITTS_IGEMM_256");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int TN, int WAVES_M, int WAVES_N, int BK, int NSLOT, typename OutT>
+void launch256(const IgArgs& a, hipStream_t s) {
+  dim3 grid(((a.Tmax + 255) / 256) * ((a.Cout + TN - 1) / TN) * a.B);
+  const size_t lds = (size_t)NSLOT * (256 + TN) * 2 * BK;
+  hipLaunchKernelGGL((igemm256_kernel<TN, WAVES_M, WAVES_N, BK, NSLOT, OutT>), grid, dim3(512), lds, s, a);
+}
+// tile variant (ITTS_IG256_VARIANT, A/B; profiles/ubench_igemm256_r03.txt): 0 = K steps of 32 (64-B rows),
+// 4-slot ring, 3 steps in flight; 1 = 256 x 128, K steps of 64, 3 slots; 2 = 256 x 256 K steps of 64
+// (whole 128-B lines), double-buffered, 256 x 128 of 32 for Cout % 256 != 0; 3 (default) = K steps of 64
+// double-buffered for both tile widths.  Whole lines beat depth: latent GEMMs 600 / 872 / 771 / 487
+// TF/s (v2) vs 573 / 787 / 721 / 461 (v0) vs 529 / 634 / 579 / 337 for the 128-row register-staged tile.
+int ig256_variant() {
+  static const int v = [] {
+    const char* e = getenv("ITTS_IG256_VARIANT");
+    return e ? atoi(e) : 3;
+  }();
+  return v;
+}
+
 // ITTS_IGEMM_WIN=0 keeps the per-tap A tiles (A/B measurements)
 bool igemm_win_enabled() {
   static const bool on = [] {
@@ -299,6 +552,27 @@ void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
   // Cout = 192 (stage 2): 64-column tiles instead of a half-empty second 128-column tile; in the
   // window form 256 x 64 tiles of 8 x (64 x 32) (conv k = 11: 1247 -> 912 us, profiles/igemm_ab_r02.txt)
   const bool win = vec && a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled();
+  // 256-row LDS-DMA tiles: 16-B aligned rows, 64-channel chunks, Cout a multiple of 128 (>= 256)
+  const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool g256 = vec && a.ci_pad % 32 == 0 && a.Cout >= 256 && a.Cout % 128 == 0 && a.ldx % 8 == 0 &&
+                    a.sxb % 8 == 0 && al16(a.x) && a.ldy % 8 == 0 && a.syb % 8 == 0 && al16(a.y) &&
+                    (!a.r1 || al16(a.r1)) && (!a.r2 || al16(a.r2)) && igemm256_enabled();
+  if (g256) {
+    const int v = ig256_variant();
+    const bool k64 = a.ci_pad % 64 == 0;
+    if (v == 1 && k64) launch256<128, 4, 2, 64, 3, OutT>(a, s);
+    else if (v == 3 && k64) {
+      if (a.Cout % 256 == 0) launch256<256, 2, 4, 64, 2, OutT>(a, s);
+      else launch256<128, 4, 2, 64, 2, OutT>(a, s);
+    } else if (v == 0 || !k64) {
+      if (a.Cout % 256 == 0) launch256<256, 2, 4, 32, 4, OutT>(a, s);
+      else launch256<128, 4, 2, 32, 4, OutT>(a, s);
+    } else {  // default (2): whole 128-B rows, double-buffered
+      if (a.Cout % 256 == 0) launch256<256, 2, 4, 64, 2, OutT>(a, s);
+      else launch256<128, 4, 2, 32, 4, OutT>(a, s);
+    }
+    return;
+  }
   if (wide_n && wide_k && a.Cout % 128 == 0) {
     if (win) launch_cfg<ITTS_IG_WIDEW, OutT>(a, vec, s);
     else launch_cfg<ITTS_IG_WIDE, OutT>(a, vec, s);

@@ -15,6 +15,7 @@ from indextts.utils.synthetic import gpt_state_dict
 
 cfg = load_config(default_config_path())
 eng = HipGPT(gpt_state_dict(cfg.gpt, seed=0, mel_head_std=0.08), cfg.gpt, "cuda", "bf16", max_kv=600)
+eng.cseq = False  # per-launch timing needs the Python launch sequence (same kernels as the C call)
 B = 32
 g = np.random.default_rng(0)
 conds = torch.from_numpy(g.normal(0, 1, (B, 32, 1024)).astype(np.float32)).cuda()
