@@ -278,7 +278,7 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int TN, int WAVES_M, int WAVES_N, int BK, int NSLOT, typename OutT>
+template <int TN, int WAVES_M, int WAVES_N, int BK, int NSLOT, typename OutT, bool WIN = false>
 __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
   constexpr int TM = 256, ROWB = BK * 2, SPR = BK / 8, RPI = 1024 / ROWB;  // 16-B slots per row, rows per DMA
   constexpr int D = NSLOT - 1;  // K steps in flight ahead of the one computed
@@ -287,8 +287,14 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
   constexpr int A_INS = TM / RPI / 8, B_INS = TN / RPI / 8;  // DMA instructions per wave per K step
   constexpr int P = A_INS + B_INS;
   constexpr int EP = WN + 4;  // epilogue staging pitch (floats): rows r and r + 4 on other banks
+  // WIN (convs of >= 3 taps): K steps run channel chunk outer, tap inner; a chunk's A operand is ONE
+  // window of TM + kWinSpan input rows, in its own double buffer, and a K step moves only B.  The next
+  // chunk's window is issued at the first step of a chunk, after that step's B, so it may stay in flight
+  // across one barrier (counted vmcnt) and lands during the chunk's taps.
+  constexpr int WROWS = TM + kWinSpan, W_BYTES = WROWS * ROWB, W_INS = WROWS / RPI / 8;
   static_assert(WAVES_M * WAVES_N == 8 && B_INS >= 1 && (BK == 32 || BK == 64) && D >= 1, "geometry");
-  static_assert(8 * 32 * EP * 4 <= NSLOT * STAGE, "epilogue staging fits the ring");
+  static_assert(!WIN || (NSLOT == 2 && WROWS % (RPI * 8) == 0), "window form: double-buffered B");
+  static_assert(8 * 32 * EP * 4 <= (WIN ? 2 * (W_BYTES + B_BYTES) : NSLOT * STAGE), "epilogue staging fits");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // slot permutation of a row (an involution on the row's SPR slots): 16 consecutive rows of a fragment
   // read fall on 16 distinct bank quads
@@ -314,6 +320,34 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
   // DMA of K step it into ring slot it % NSLOT: lane l of an instruction covers row R + l / SPR,
   // physical slot l % SPR = logical slot (l % SPR) ^ swz(row)
   const int lr = lane / SPR, ls = lane % SPR;
+  // WIN: [window 0][window 1][B 0][B 1]
+  auto issue_win = [&](int c) {
+    const int c0 = c * BK;
+    unsigned char* Ws = smem + (c & 1) * W_BYTES;
+#pragma unroll
+    for (int i = 0; i < W_INS; ++i) {
+      const int R = (wave * W_INS + i) * RPI, row = R + lr;
+      const int s = ls ^ swz(row);
+      const int t = q0 + row + p.min_off, cc = c0 + 8 * s;
+      const void* src = (t >= 0 && t < len && cc < p.Cin) ? static_cast<const void*>(X + (int64_t)t * p.ldx + cc)
+                                                          : static_cast<const void*>(g_zero_line);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(Ws + R * ROWB), 16, 0, 0);
+    }
+  };
+  auto issue_b = [&](int it) {
+    const int c = it / p.ntaps, j = it - c * p.ntaps;
+    unsigned char* Bs = smem + 2 * W_BYTES + (it & 1) * B_BYTES;
+    const uint16_t* Wj = p.w + (int64_t)j * p.co_pad * p.ci_pad + c * BK;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      const int R = (wave * B_INS + i) * RPI, row = R + lr;
+      const int s = ls ^ swz(row);
+      const int n = n0 + row;
+      const void* src = n < p.co_pad ? static_cast<const void*>(Wj + (int64_t)n * p.ci_pad + 8 * s)
+                                     : static_cast<const void*>(g_zero_line);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(Bs + R * ROWB), 16, 0, 0);
+    }
+  };
   auto issue = [&](int it) {
     const int j = it / nchunks, c0 = (it - j * nchunks) * BK;
     const int toff = p.tap_off[j];
@@ -358,12 +392,19 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
   auto compute = [&](int it) {
     const unsigned char* As = smem + (it % NSLOT) * STAGE;
     const unsigned char* Bs = As + A_BYTES;
+    int arow = 0;  // WIN: this tap's first window row
+    if constexpr (WIN) {
+      const int c = it / p.ntaps, j = it - c * p.ntaps;
+      As = smem + (c & 1) * W_BYTES;
+      Bs = smem + 2 * W_BYTES + (it & 1) * B_BYTES;
+      arow = p.tap_off[j] - p.min_off;
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8_t af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int row = wm + 32 * i + r32;
+        const int row = arow + wm + 32 * i + r32;
         af[i] = *reinterpret_cast<const bf16x8_t*>(As + row * ROWB + (((2 * ks + h) ^ swz(row)) << 4));
       }
 #pragma unroll
@@ -377,18 +418,35 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
-  // prologue: steps 0 .. D-1 in flight, step 0 retired
-#pragma unroll
-  for (int k = 0; k < D; ++k)
-    if (k < kiters) issue(k);
-  retire_next(-1);
-  lds_barrier();
-  for (int it = 0; it < kiters; ++it) {
-    // slot (it + D) % NSLOT was last read in step it - 1, which every wave finished before the last barrier
-    if (it + D < kiters) issue(it + D);
-    compute(it);
-    retire_next(it);
+  if constexpr (WIN) {
+    issue_win(0);
+    issue_b(0);
+    wait_vm<0>();
     lds_barrier();
+    for (int it = 0; it < kiters; ++it) {
+      const int c = it / p.ntaps, j = it - c * p.ntaps;
+      const bool nextwin = j == 0 && (c + 1) * BK < p.ci_pad;
+      if (it + 1 < kiters) issue_b(it + 1);  // B slot (it + 1) & 1 was last read in step it - 1
+      if (nextwin) issue_win(c + 1);          // window slot (c + 1) & 1 was last read in chunk c - 1
+      compute(it);
+      if (nextwin) wait_vm<W_INS>();  // B(it + 1) retired; the window stays in flight one more step
+      else wait_vm<0>();
+      lds_barrier();
+    }
+  } else {
+    // prologue: steps 0 .. D-1 in flight, step 0 retired
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+      if (k < kiters) issue(k);
+    retire_next(-1);
+    lds_barrier();
+    for (int it = 0; it < kiters; ++it) {
+      // slot (it + D) % NSLOT was last read in step it - 1, which every wave finished before the last barrier
+      if (it + D < kiters) issue(it + D);
+      compute(it);
+      retire_next(it);
+      lds_barrier();
+    }
   }
 
   // ---- epilogue: per 32-row band, f32 rows through this wave's LDS staging, 16-B row accesses
@@ -484,9 +542,18 @@ bool igemm256_enabled() {
   return on;
 }
 
+bool igemm_win_enabled();
+
 template <int TN, int WAVES_M, int WAVES_N, int BK, int NSLOT, typename OutT>
 void launch256(const IgArgs& a, hipStream_t s) {
   dim3 grid(((a.Tmax + 255) / 256) * ((a.Cout + TN - 1) / TN) * a.B);
+  if constexpr (NSLOT == 2 && BK == 64) {
+    if (a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled()) {
+      const size_t lds = 2 * (size_t)(256 + kWinSpan + TN) * 2 * BK;
+      hipLaunchKernelGGL((igemm256_kernel<TN, WAVES_M, WAVES_N, BK, 2, OutT, true>), grid, dim3(512), lds, s, a);
+      return;
+    }
+  }
   const size_t lds = (size_t)NSLOT * (256 + TN) * 2 * BK;
   hipLaunchKernelGGL((igemm256_kernel<TN, WAVES_M, WAVES_N, BK, NSLOT, OutT>), grid, dim3(512), lds, s, a);
 }
