@@ -612,6 +612,9 @@ void launch_cfg(const IgArgs& a, bool vec, hipStream_t s) {
 #define ITTS_IG_WIDEW ITTS_IG_WIDE
 #endif
 template <typename OutT>
+void dispatch_old(const IgArgs& a, bool vec, hipStream_t s);
+
+template <typename OutT>
 void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
   const bool wide_n = a.Cout >= 128, wide_k = a.Cin >= 128;
   // wide layers: 8 waves per 128 x 128 tile (64 x 32 each) -- more waves per CU to hide the staging
@@ -621,12 +624,17 @@ void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
   const bool win = vec && a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled();
   // 256-row LDS-DMA tiles: 16-B aligned rows, 64-channel chunks, Cout a multiple of 128 (>= 256)
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  const bool g256 = vec && a.ci_pad % 32 == 0 && a.Cout >= 256 && a.Cout % 128 == 0 && a.ldx % 8 == 0 &&
+  const bool g256 = vec && a.ci_pad % 32 == 0 && a.Cout >= 192 && a.Cout % 64 == 0 && a.ldx % 8 == 0 &&
                     a.sxb % 8 == 0 && al16(a.x) && a.ldy % 8 == 0 && a.syb % 8 == 0 && al16(a.y) &&
                     (!a.r1 || al16(a.r1)) && (!a.r2 || al16(a.r2)) && igemm256_enabled();
   if (g256) {
     const int v = ig256_variant();
     const bool k64 = a.ci_pad % 64 == 0;
+    if (a.Cout % 128 != 0) {  // Cout = 192 (generator stage 2): 256 x 64 tiles, 4 x 2 waves of 64 x 32
+      if (k64) launch256<64, 4, 2, 64, 2, OutT>(a, s);
+      else dispatch_old<OutT>(a, vec, s);
+      return;
+    }
     if (v == 1 && k64) launch256<128, 4, 2, 64, 3, OutT>(a, s);
     else if (v == 3 && k64) {
       if (a.Cout % 256 == 0) launch256<256, 2, 4, 64, 2, OutT>(a, s);
@@ -640,6 +648,14 @@ void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
     }
     return;
   }
+  dispatch_old<OutT>(a, vec, s);
+}
+
+// the register-staged 128 / 256-row tiles (layers the LDS-DMA tile does not take)
+template <typename OutT>
+void dispatch_old(const IgArgs& a, bool vec, hipStream_t s) {
+  const bool wide_n = a.Cout >= 128, wide_k = a.Cin >= 128;
+  const bool win = vec && a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled();
   if (wide_n && wide_k && a.Cout % 128 == 0) {
     if (win) launch_cfg<ITTS_IG_WIDEW, OutT>(a, vec, s);
     else launch_cfg<ITTS_IG_WIDE, OutT>(a, vec, s);
