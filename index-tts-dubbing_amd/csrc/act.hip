@@ -185,8 +185,14 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
 // loaded), replicate-clamped per utterance.  Interior outputs leave straight from the down product's
 // accumulators (8-B stores of 4 channels); outputs within 3 samples of an utterance edge, where the
 // down-sampler's own replicate pad applies, are recomputed by the VALU formula from the same window.
+#ifndef ITTS_ACT_TAPS_LDS  // the FIR operands in LDS instead of 56 VGPRs per lane
+#define ITTS_ACT_TAPS_LDS 0  // measured neutral (profiles/ubench_act_r03.txt): the taps are not what holds the registers
+#endif
 template <int NB, int S>
-__global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p, int ntt, int njobs) {
+#ifndef ITTS_ACT_WPS  // waves per SIMD the register allocation targets
+#define ITTS_ACT_WPS 2  // 3 spills 32-37 VGPRs: 30-40 % slower (profiles/ubench_act_r03.txt)
+#endif
+__global__ __launch_bounds__(256, ITTS_ACT_WPS) void aa_snake_mfma_kernel(ActArgs p, int ntt, int njobs) {
   constexpr int PX = NB * 64, NS = 4 / NB, TT = NS * 32 * S, WROWS = TT + 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char win[];
   const int c0 = blockIdx.x * NB * 32;
@@ -194,6 +200,7 @@ __global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p, int ntt, 
   constexpr int CV = NB * 4;  // 16-B vectors per row
   constexpr int NV = (WROWS * CV + 255) / 256;
   float* tl = reinterpret_cast<float*>(win + WROWS * PX);  // 12 up taps, 12 down taps
+  bf16x8_t* tap_lds = reinterpret_cast<bf16x8_t*>(win + WROWS * PX + 128);  // 16-B aligned (PX % 64 == 0)
   if (tid < 24) tl[tid] = tid < 12 ? p.up[tid] : p.down[tid - 12];
 
   // window rows 1 .. TT + 12 (t0 - 6 .. t0 + TT + 5) of job j into registers
@@ -219,8 +226,13 @@ __global__ __launch_bounds__(256) void aa_snake_mfma_kernel(ActArgs p, int ntt, 
 
   const int blk = wave % NB, sidx = wave / NB;
   const int cb = 32 * blk;  // window column of the block
+#if ITTS_ACT_TAPS_LDS
+  itts_actm::store_taps(tl, tap_lds);  // visible after the barrier at the first job's window store
+  const itts_actm::TapsL T{tap_lds};
+#else
   itts_actm::Taps T;
   itts_actm::make_taps(tl, T);
+#endif
   const int ch = c0 + cb + (lane & 31);
   const float a_rev = ch < p.C ? expf(p.log_alpha[ch]) * 0.15915494309189535f : 0.f;
   const float inv_b = ch < p.C ? 1.0f / (expf(p.log_beta[ch]) + 1e-9f) : 0.f;
@@ -282,7 +294,7 @@ void launch_mfma(const ActArgs& a, hipStream_t s) {
   const int ntt = (a.T + TT - 1) / TT, njobs = ntt * a.B;
   int per = ITTS_ACT_WGS / ngrp;
   per = per < 1 ? 1 : (per > njobs ? njobs : per);
-  const size_t lds = (size_t)(TT + 32) * NB * 64 + 24 * sizeof(float);
+  const size_t lds = (size_t)(TT + 32) * NB * 64 + 128 + (ITTS_ACT_TAPS_LDS ? itts_actm::kTapsLdsBytes : 0);
   hipLaunchKernelGGL((aa_snake_mfma_kernel<NB, S>), dim3(ngrp, per, 1), dim3(256), lds, s, a, ntt, njobs);
 }
 

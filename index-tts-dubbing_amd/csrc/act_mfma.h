@@ -40,9 +40,21 @@ typedef __attribute__((ext_vector_type(8))) short v8s;
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 struct Taps {
-  bf16x8_t fu[2][2];  // up F (A operand):    [K-block][hi, lo]
-  bf16x8_t gd[5][2];  // down G^T (B operand): [K-block][hi, lo]
+  bf16x8_t fu_[2][2];  // up F (A operand):    [K-block][hi, lo]
+  bf16x8_t gd_[5][2];  // down G^T (B operand): [K-block][hi, lo]
+  __device__ __forceinline__ bf16x8_t fu(int kb, int hl) const { return fu_[kb][hl]; }
+  __device__ __forceinline__ bf16x8_t gd(int kk, int hl) const { return gd_[kk][hl]; }
 };
+// The same 14 lane-dependent operands kept in LDS ([14][64 lanes] x 16 B, written once per workgroup by
+// store_taps) and read at their MFMA: 56 VGPRs fewer per wave than Taps in registers.
+struct TapsL {
+  const bf16x8_t* p;  // LDS
+  __device__ __forceinline__ bf16x8_t fu(int kb, int hl) const { return p[(2 * kb + hl) * 64 + (threadIdx.x & 63)]; }
+  __device__ __forceinline__ bf16x8_t gd(int kk, int hl) const {
+    return p[(4 + 2 * kk + hl) * 64 + (threadIdx.x & 63)];
+  }
+};
+constexpr int kTapsLdsBytes = 14 * 64 * 16;
 
 __device__ __forceinline__ __bf16 hi_part(float v) { return (__bf16)v; }
 __device__ __forceinline__ __bf16 lo_part(float v) { return (__bf16)(v - (float)(__bf16)v); }
@@ -65,8 +77,8 @@ __device__ inline void make_taps(const float* tl, Taps& T) {
       const int idx = ok ? (odd ? 6 - 2 * q : 5 - 2 * q) : 0;
       const float t = tl[idx];
       const float v = ok ? 2.0f * t : 0.f;
-      T.fu[kb][0][e] = hi_part(v);
-      T.fu[kb][1][e] = lo_part(v);
+      T.fu_[kb][0][e] = hi_part(v);
+      T.fu_[kb][1][e] = lo_part(v);
     }
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk)
@@ -77,9 +89,25 @@ __device__ inline void make_taps(const float* tl, Taps& T) {
       const bool ok = idx >= 0 && idx < 12;
       const float t = tl[12 + (ok ? idx : 0)];
       const float v = ok ? t : 0.f;
-      T.gd[kk][0][e] = hi_part(v);
-      T.gd[kk][1][e] = lo_part(v);
+      T.gd_[kk][0][e] = hi_part(v);
+      T.gd_[kk][1][e] = lo_part(v);
     }
+}
+
+// wave 0 of the workgroup builds the taps and stores them for TapsL (caller: barrier before use)
+__device__ inline void store_taps(const float* tl, bf16x8_t* lds) {
+  if ((threadIdx.x >> 6) != 0) return;
+  Taps T;
+  make_taps(tl, T);
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) lds[(2 * kb + hl) * 64 + lane] = T.fu_[kb][hl];
+#pragma unroll
+  for (int kk = 0; kk < 5; ++kk)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) lds[(4 + 2 * kk + hl) * 64 + lane] = T.gd_[kk][hl];
 }
 
 __device__ __forceinline__ float snake_rev(float u, float a_rev, float inv_b) {
@@ -101,8 +129,8 @@ __device__ __forceinline__ int woff(int row, int ch) {
 
 // U tile: 32 up-sampled positions x 32 channels from input rows row0 .. row0+31, channels cb ..
 // cb+31 of the window (EXEC must be full: the transposed read gathers across lanes)
-template <int PX>
-__device__ __forceinline__ f32x16_t up_tile(const unsigned char* win, int row0, int cb, const Taps& T) {
+template <int PX, class TT>
+__device__ __forceinline__ f32x16_t up_tile(const unsigned char* win, int row0, int cb, const TT& T) {
   const int lane = threadIdx.x & 63, li = lane & 15, h = lane >> 5;
   const int q = li >> 2, p = li & 3;
   const int col = cb + 16 * ((lane >> 4) & 1) + 4 * p;
@@ -116,8 +144,8 @@ __device__ __forceinline__ f32x16_t up_tile(const unsigned char* win, int row0, 
     const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(win + woff<PX>(r + 4, col)));
     const v8s b8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     const bf16x8_t b = __builtin_bit_cast(bf16x8_t, b8);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(T.fu[kb][0], b, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(T.fu[kb][1], b, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(T.fu(kb, 0), b, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(T.fu(kb, 1), b, acc, 0, 0, 0);
   }
   return acc;
 }
@@ -135,11 +163,11 @@ __device__ __forceinline__ void snake_pack(const f32x16_t& u, float a_rev, float
 // One strip: outputs t0 + [0, 32 ntile) for channels cb .. cb+31.  `row0` = window row of time
 // t0 - 7.  emit(i, acc): acc = Y^T of output tile i, lane (h, n) holding output time t0 + 32 i + n
 // and channels cb + 8 g + 4 h + (0..3) in acc[4 g .. 4 g + 3].
-template <int PX, class Emit>
-__device__ __forceinline__ void strip(const unsigned char* win, int row0, int cb, int ntile, const Taps& T,
+template <int PX, class TT, class Emit>
+__device__ __forceinline__ void strip(const unsigned char* win, int row0, int cb, int ntile, const TT& T,
                                       float a_rev, float inv_b, Emit&& emit) {
   bf16x8_t c0, c1;
-  snake_pack(up_tile<PX>(win, row0, cb, T), a_rev, inv_b, c0, c1);
+  snake_pack(up_tile<PX>(win, row0, cb, T), a_rev, inv_b, c0, c1);  // T: Taps or TapsL
   for (int i = 0; i < ntile; ++i) {
     bf16x8_t b2, b3, b4, b5;
     snake_pack(up_tile<PX>(win, row0 + 32 * i + 16, cb, T), a_rev, inv_b, b2, b3);
@@ -150,8 +178,8 @@ __device__ __forceinline__ void strip(const unsigned char* win, int row0, int cb
     const bf16x8_t blk[5] = {c0, c1, b2, b3, b4};
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(blk[kk], T.gd[kk][0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(blk[kk], T.gd[kk][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(blk[kk], T.gd(kk, 0), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(blk[kk], T.gd(kk, 1), acc, 0, 0, 0);
     }
     emit(i, acc);
     c0 = b4;

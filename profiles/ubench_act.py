@@ -10,7 +10,7 @@ from indextts.utils.synthetic import kaiser_sinc_lowpass
 
 lib = _hip.load()
 B, N = 32, int(os.environ.get("N", "20"))
-shapes = [(768, 1600), (384, 6400), (192, 25600), (96, 102400), (24, 409600)]
+shapes = [(768, 1600), (384, 6400), (192, 25600), (96, 102400), (48, 204800), (24, 409600)]
 if len(sys.argv) > 1:
     shapes = [s for s in shapes if str(s[0]) in sys.argv[1:]]
 f = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).cuda()
