@@ -144,6 +144,12 @@ int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* latent, const 
  * infer.py:509-514).  n_fft a power of two <= 2048, L > n_fft/2. */
 int itts_log_mel(const float* audio, int64_t ld_audio, int B, int L, const float* window, const float* mel_fb,
                  int n_fft, int hop, int n_mels, float* out, void* stream);
+/* Band-limited resampling of the prompt (torchaudio.functional.resample, sinc_interp_hann: the
+ * reference's Resample(sr, 24000), infer.py:509-514): rates reduced by their gcd to orig : new_rate,
+ * kern [new_rate][2*width + orig] the windowed-sinc table (f32), y[b][i] for i < Lout,
+ * y[new*f + p] = sum_k x[orig*f + k - width] * kern[p][k] (zero outside [0, L)). */
+int itts_resample_sinc(const float* x, int64_t ldx, int B, int L, const float* kern, int orig, int new_rate,
+                       int width, float* y, int64_t ldy, int Lout, void* stream);
 
 /* ---- GPT (UnifiedVoice + HF GPT-2) ------------------------------------------------------------ */
 

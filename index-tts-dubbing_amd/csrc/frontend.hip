@@ -73,3 +73,46 @@ extern "C" int itts_log_mel(const float* audio, int64_t ld_audio, int B, int L, 
                      window, mel_fb, n_fft, hop, n_mels, n_frames, out);
   return itts::check_launch(fn);
 }
+
+// ---- band-limited resampling (torchaudio.functional.resample, sinc_interp_hann) -------------------
+// Reference: infer.py:509-514 (torchaudio.transforms.Resample(sr, 24000) of the prompt).  With the
+// rates reduced by their gcd to orig : new, output i = new * f + p (frame f, phase p) is
+//   y[i] = sum_{k < K} xpad[orig * f + k] * kern[p][k],   xpad[j] = x[j - width] (zero outside [0, L)),
+// K = 2 * width + orig; kern is the windowed-sinc table built on the host (utils/audio.py
+// sinc_resample_kernel, float64 -> f32).  One thread per output sample, taps in k order (fixed
+// rounding); the table rows are L1/L2-resident (a few KB to ~100 KB).
+namespace {
+__global__ __launch_bounds__(256) void resample_kernel(const float* __restrict__ x, int64_t ldx, int L,
+                                                       const float* __restrict__ kern, int orig, int nw, int width,
+                                                       float* __restrict__ y, int64_t ldy, int Lout) {
+  const int i = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (i >= Lout) return;
+  const int K = 2 * width + orig;
+  const int f = i / nw, ph = i - f * nw;
+  const float* xr = x + (int64_t)b * ldx;
+  const float* kr = kern + (int64_t)ph * K;
+  const int j0 = orig * f - width;  // x index of tap 0
+  float acc = 0.f;
+  if (j0 >= 0 && j0 + K <= L) {
+    for (int k = 0; k < K; ++k) acc = fmaf(xr[j0 + k], kr[k], acc);
+  } else {
+    for (int k = 0; k < K; ++k) {
+      const int j = j0 + k;
+      if (j >= 0 && j < L) acc = fmaf(xr[j], kr[k], acc);
+    }
+  }
+  y[(int64_t)b * ldy + i] = acc;
+}
+}  // namespace
+
+extern "C" int itts_resample_sinc(const float* x, int64_t ldx, int B, int L, const float* kern, int orig, int new_rate,
+                                  int width, float* y, int64_t ldy, int Lout, void* stream) {
+  const char* fn = "itts_resample_sinc";
+  ITTS_REQUIRE(B >= 0 && L >= 0 && Lout >= 0 && orig > 0 && new_rate > 0 && width >= 0, fn, "bad sizes");
+  if (B == 0 || Lout == 0) return 0;
+  ITTS_REQUIRE(x && kern && y, fn, "null pointer");
+  ITTS_REQUIRE((int64_t)(Lout - 1) / new_rate * orig + 2 * width + orig < (int64_t)1 << 31, fn, "too long");
+  hipLaunchKernelGGL(resample_kernel, dim3((Lout + 255) / 256, B), dim3(256), 0, itts::as_stream(stream), x, ldx, L,
+                     kern, orig, new_rate, width, y, ldy, Lout);
+  return itts::check_launch(fn);
+}

@@ -13,6 +13,8 @@
 //    prompt block, and the teacher-forced latent pass); optionally writes K/V into the decode cache.
 //    bf16 mode: MFMA flash attention (attn_prefill_mfma_kernel); f32 verification mode: one thread
 //    per query, K/V staged through LDS in 32-key blocks, exact-f32 block-wise online softmax.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -77,7 +79,7 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 #ifndef ITTS_KV_NT
 #define ITTS_KV_NT 1
 #endif
-template <typename TC, typename TO, int NT, bool ROWS, bool PROJ>
+template <typename TC, typename TO, int NT, bool ROWS, bool PROJ, int KB = ITTS_ATTN_KB>
 __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
                                                          int64_t split_stride, const float* __restrict__ qkv_bias,
                                                          TC* __restrict__ cache_k, TC* __restrict__ cache_v,
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
                                                          float* __restrict__ part, int64_t part_stride, int64_t ldp) {
   static_assert(!PROJ || NT == 256, "the c_proj epilogue maps 256 threads onto 2 x 128 column slots");
   constexpr int NG = NT / 8;
-  constexpr int KB = ITTS_ATTN_KB;               // keys per group per round (packed rows in registers)
+  // KB: keys per group per round (packed rows in registers)
   constexpr int RW = sizeof(TC) * 8 / 16;       // 16-B vectors per lane per row (bf16: 1, f32: 2)
   __shared__ float qs[kHD], kn[kHD], vn[kHD];
   __shared__ float gm[NG], gl[NG];
@@ -579,16 +581,29 @@ int attn_decode_launch(const char* fn, const float* qkv, int64_t ldqkv, int nspl
   dim3 grid(H, B);
   hipStream_t s = itts::as_stream(stream);
   const uint16_t* wp = static_cast<const uint16_t*>(wproj);
-#define ITTS_AD(TC, TO, PR)                                                                                         \
+  // keys per group per round: 10 (320 keys per workgroup round) for the 32-row steps, 4 for steps of
+  // >= 128 rows (long-form chunks), whose 2048+ workgroups are occupancy-bound at 10 -- B = 128: S = 71
+  // 23.8 -> 15.5 us, S = 300 31.1 vs 31.7 (profiles/ubench_attn_kb_r03.txt)
+  static const bool small_ok = [] {  // ITTS_ATTN_SMALLKB=0: always 10 (A/B)
+    const char* e = getenv("ITTS_ATTN_SMALLKB");
+    return !(e && e[0] == '0');
+  }();
+  const bool small_kb = small_ok && B >= 128 && !wproj;
+#define ITTS_AD1(TC, TO, PR, KBV)                                                                                     \
   do {                                                                                                            \
     if (kv_rows)                                                                                                  \
-      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, true, PR>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,   \
-                         split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base,      \
-                         tstate, (TO*)out, ldo, H, kv_rows, ld_rows, wp, N, part, part_stride, ldp);                \
+      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, true, PR, KBV>), grid, dim3(256), 0, s, qkv, ldqkv,      \
+                         nsplit, split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad,       \
+                         kv_base, tstate, (TO*)out, ldo, H, kv_rows, ld_rows, wp, N, part, part_stride, ldp);       \
     else                                                                                                          \
-      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, false, PR>), grid, dim3(256), 0, s, qkv, ldqkv, nsplit,  \
-                         split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad, kv_base,      \
-                         tstate, (TO*)out, ldo, H, nullptr, 0, wp, N, part, part_stride, ldp);                      \
+      hipLaunchKernelGGL((attn_decode_kernel<TC, TO, 256, false, PR, KBV>), grid, dim3(256), 0, s, qkv, ldqkv,     \
+                         nsplit, split_stride, qkv_bias, (TC*)cache_k, (TC*)cache_v, cache_bs, cache_hs, pad,       \
+                         kv_base, tstate, (TO*)out, ldo, H, nullptr, 0, wp, N, part, part_stride, ldp);             \
+  } while (0)
+#define ITTS_AD(TC, TO, PR)                  \
+  do {                                       \
+    if (!PR && small_kb) ITTS_AD1(TC, TO, false, 4); \
+    else ITTS_AD1(TC, TO, PR, ITTS_ATTN_KB); \
   } while (0)
   if (wproj) {
     if (cache_dtype == ITTS_BF16) ITTS_AD(uint16_t, float, true);
@@ -603,6 +618,7 @@ int attn_decode_launch(const char* fn, const float* qkv, int64_t ldqkv, int nspl
     ITTS_AD(float, uint16_t, false);
   }
 #undef ITTS_AD
+#undef ITTS_AD1
   return itts::check_launch(fn);
 }
 }  // namespace

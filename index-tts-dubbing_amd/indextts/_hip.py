@@ -43,6 +43,7 @@ SIGNATURES = {
     "itts_conv_post_tanh":(_c_i, [_vp, _c_i64, _c_i64, _vp, _c_f, _c_i, _c_i, _vp, _c_i, _c_i, _vp, _vp, _c_i64,
                                    _c_i, _vp]),
     "itts_log_mel": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _vp, _c_i, _c_i, _c_i, _vp, _vp]),
+    "itts_resample_sinc": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _c_i, _c_i, _c_i, _vp, _c_i64, _c_i, _vp]),
     "itts_layernorm_rows": (_c_i, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp, _vp, _vp, _c_i, _vp]),
     "itts_residual_reduce_ln": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp,
                                        _vp, _vp, _c_i, _vp]),

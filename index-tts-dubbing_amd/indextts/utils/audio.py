@@ -80,6 +80,24 @@ def resample(wav: torch.Tensor, orig_sr: int, new_sr: int) -> torch.Tensor:
     return y[..., :target].reshape(*shape[:-1], -1)
 
 
+def resample_hip(wav: torch.Tensor, orig_sr: int, new_sr: int) -> torch.Tensor:
+    """``resample`` on the GPU (itts_resample_sinc, csrc/frontend.hip): wav [..., L] f32 on a HIP device."""
+    from .. import _hip
+    if orig_sr == new_sr:
+        return wav
+    k, o, n, width = sinc_resample_kernel(orig_sr, new_sr)
+    shape = wav.shape
+    x = wav.reshape(-1, shape[-1]).float().contiguous()
+    B, L = x.shape
+    target = math.ceil(n * L / o)
+    kern = k.reshape(n, -1).to(wav.device, torch.float32).contiguous()
+    y = torch.empty(B, target, dtype=torch.float32, device=wav.device)
+    lib = _hip.load()
+    _hip.check(lib.itts_resample_sinc(x.data_ptr(), x.stride(0), B, L, kern.data_ptr(), o, n, width, y.data_ptr(),
+                                      y.stride(0), target, _hip.stream_ptr(wav.device)), "itts_resample_sinc")
+    return y.reshape(*shape[:-1], target)
+
+
 def mel_filterbank(n_freqs: int, f_min: float, f_max: float, n_mels: int, sr: int) -> torch.Tensor:
     """HTK triangular filterbank [n_freqs, n_mels] (no area normalisation)."""
     all_f = torch.linspace(0, sr // 2, n_freqs)
@@ -140,14 +158,13 @@ def log_mel_hip(audio: torch.Tensor, feats: "MelSpectrogramFeatures" = None) -> 
 
 def prompt_mel(path: str, device=None) -> torch.Tensor:
     """The prompt-mel pipeline of ``infer()`` (``indextts/infer.py:509-514``) -> [1, 100, frames].
-    ``device`` (a HIP device): resampling and the log-mel run there (the mel on the HIP kernel);
+    ``device`` (a HIP device): resampling and the log-mel run there on the HIP kernels
+    (itts_resample_sinc, itts_log_mel);
     None: the CPU restatement (used by the tests as the from-spec reference)."""
     audio, sr = load_wav(path)
     audio = torch.mean(audio, dim=0, keepdim=True)
     if device is not None and torch.device(device).type == "cuda":
         audio = audio.to(device)
-        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
-            audio = resample(audio, sr, 24000)
-        return log_mel_hip(audio)
+        return log_mel_hip(resample_hip(audio, sr, 24000))
     audio = resample(audio, sr, 24000)
     return MelSpectrogramFeatures()(audio)
