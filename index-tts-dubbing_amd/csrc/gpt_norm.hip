@@ -8,6 +8,8 @@
 //       x[b] += bias + sum_s part[s][b]          (deterministic fixed-order sum, no atomics)
 //       h[b]  = LN2?(LN1(x[b]))                 (input of the next projection GEMM)
 // One 256-thread workgroup per row; two-pass (mean, then centred variance) in f32 like torch.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -105,7 +107,8 @@ __global__ __launch_bounds__(1024) void residual_reduce_ln_v4_kernel(
     const float* __restrict__ bias, TO* __restrict__ h, int64_t ldh, int D, const float* g1, const float* b1,
     const float* g2, const float* b2) {
   __shared__ float red[16];
-  const int m = blockIdx.x, e = 4 * threadIdx.x;
+  // without LayerNorm a row is cut into gridDim.y column blocks (more workgroups per launch)
+  const int m = blockIdx.x, e = 4 * (blockIdx.y * blockDim.x + threadIdx.x);
   float* xr = x + (int64_t)m * ldx + e;
   f32x4_t acc = *reinterpret_cast<const f32x4_t*>(xr);
   f32x4_t pv[kMaxSplit];
@@ -209,11 +212,20 @@ extern "C" int itts_residual_reduce_ln(float* x, int64_t ldx, const float* part,
   const bool v4 = D % 256 == 0 && D <= 4096 && nsplit <= kMaxSplit && ldx % 4 == 0 && ldp % 4 == 0 &&
                   split_stride % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(part)) & 15) == 0;
   if (v4) {
+    // no LayerNorm: 64-thread column blocks of 256 elements, M x D/256 workgroups (32 rows: 128 instead of
+    // 32 workgroups of one row each -- the partial rows stream from 4x the CUs); ITTS_REDUCE_COLS=0: one
+    // workgroup per row (A/B)
+    static const bool cols = [] {
+      const char* e = getenv("ITTS_REDUCE_COLS");
+      return !(e && e[0] == '0');
+    }();
+    const bool split = !g1 && cols;
+    const dim3 grid(M, split ? D / 256 : 1), block(split ? 64 : D / 4);
     if (out_dtype == ITTS_BF16)
-      hipLaunchKernelGGL(residual_reduce_ln_v4_kernel<uint16_t>, dim3(M), dim3(D / 4), 0, s, x, ldx, part, nsplit,
+      hipLaunchKernelGGL(residual_reduce_ln_v4_kernel<uint16_t>, grid, block, 0, s, x, ldx, part, nsplit,
                          split_stride, ldp, bias, (uint16_t*)h, ldh, D, g1, b1, g2, b2);
     else
-      hipLaunchKernelGGL(residual_reduce_ln_v4_kernel<float>, dim3(M), dim3(D / 4), 0, s, x, ldx, part, nsplit,
+      hipLaunchKernelGGL(residual_reduce_ln_v4_kernel<float>, grid, block, 0, s, x, ldx, part, nsplit,
                          split_stride, ldp, bias, (float*)h, ldh, D, g1, b1, g2, b2);
     return itts::check_launch(fn);
   }
