@@ -72,6 +72,13 @@ int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packe
                    const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy,
                    const int32_t* lengths, int B, int Tmax, int Cin, int Cout, int ntaps, const int32_t* tap_off,
                    int y_row_mul, int y_row_off, float alpha, int gelu, int out_dtype, void* stream);
+/* Split-K form of the 1-tap igemm for long reductions over few rows (the conditioning encoder's
+ * Linear(C * F -> D) after Conv2dSubsampling2, K = 25088): x bf16 [M][ldx] (K columns), w_chunks =
+ * nsplit consecutive packed weights of the K / nsplit column chunks (each itts_igemm_pack_dims(K / nsplit,
+ * N) sized), partials f32 [nsplit][M][N] workspace, y f32 [M][N] = bias + sum of the partials in chunk
+ * order (row-independent, run-to-run identical). */
+int itts_igemm_splitk(const void* x, int64_t ldx, int M, int K, const void* w_chunks, int nsplit, int N,
+                      const float* bias, float* partials, float* y, void* stream);
 /* One AMPBlock1 conv of the narrow stages (C in {24, 48, 96} after padding to 32/64/96) with the
  * preceding Activation1d fused in (log_alpha == NULL: no activation):
  *   y[b][t][:] = alpha * (sum_j W_j . act(x)[b][t + tap_off[j]][:] + bias + r1[b][t][:] + r2[b][t][:])
@@ -150,6 +157,20 @@ int itts_log_mel(const float* audio, int64_t ld_audio, int B, int L, const float
  * y[new*f + p] = sum_k x[orig*f + k - width] * kern[p][k] (zero outside [0, L)). */
 int itts_resample_sinc(const float* x, int64_t ldx, int B, int L, const float* kern, int orig, int new_rate,
                        int width, float* y, int64_t ldy, int Lout, void* stream);
+
+/* Conditioning encoder, bf16 product path (HipGPT.conditioning(fast=True)):
+ * itts_cond_subsample -- Conv2dSubsampling2 (gpt/conformer/subsampling.py:164-190): conv2d(1 -> C, 3x3,
+ * stride 2) + ReLU of the image x[time][bin] = mel[b][bin][time] (mel strides mel_sb / mel_ld, unit time
+ * stride), out bf16 y[B][To][Fo][C], To = (T - 3) / 2 + 1, Fo = (n_bins - 3) / 2 + 1; w [C][3][3], bias [C].
+ * itts_cond_glu_dwconv -- ConvolutionModule middle (gpt/conformer_encoder.py:108-167): a [B][T][lda]
+ * (pointwise_conv1 output, 2C channels) -> GLU -> depthwise conv1d w [C][K] (+w_bias, zero padding K/2)
+ * -> LayerNorm(ln_g, ln_b, eps) -> SiLU -> bf16 y [B][T][ldy].  w_t (optional, 16-B aligned): w transposed
+ * [K][C], enables the LDS-tiled form for C = 256, 512 or 1024. */
+int itts_cond_subsample(const float* mel, int64_t mel_sb, int64_t mel_ld, int B, int n_bins, int T, const float* w,
+                        const float* bias, int C, void* y, void* stream);
+int itts_cond_glu_dwconv(const float* a, int64_t lda, int B, int T, int C, const float* w, const float* w_bias, int K,
+                         const float* ln_g, const float* ln_b, float eps, void* y, int64_t ldy, const float* w_t,
+                         void* stream);
 
 /* ---- GPT (UnifiedVoice + HF GPT-2) ------------------------------------------------------------ */
 

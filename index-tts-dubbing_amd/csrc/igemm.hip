@@ -43,6 +43,7 @@ struct IgArgs {
   const int32_t* lens;
   int B, Tmax, Cin, Cout, ci_pad, co_pad, ntaps;
   int64_t sxb, ldx, syb, ldy;
+  int64_t wsb;  // weight stride between batches (0: shared; split-K chunks: one packed chunk each)
   int ymul, yoff;
   float alpha;
   int gelu;
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
     } else {
       aload(r.a, p.tap_off[j], c0);
     }
-    const uint16_t* Wj = p.w + ((int64_t)j * p.co_pad + n0) * p.ci_pad + c0;
+    const uint16_t* Wj = p.w + b * p.wsb + ((int64_t)j * p.co_pad + n0) * p.ci_pad + c0;
 #pragma unroll
     for (int i = 0; i < B_VEC; ++i) {
       const int v = tid + NT * i, row = v / VPR, cv = (v % VPR) * 8;
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
   auto issue_b = [&](int it) {
     const int c = it / p.ntaps, j = it - c * p.ntaps;
     unsigned char* Bs = smem + 2 * W_BYTES + (it & 1) * B_BYTES;
-    const uint16_t* Wj = p.w + (int64_t)j * p.co_pad * p.ci_pad + c * BK;
+    const uint16_t* Wj = p.w + b * p.wsb + (int64_t)j * p.co_pad * p.ci_pad + c * BK;
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       const int R = (wave * B_INS + i) * RPI, row = R + lr;
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(As + R * ROWB), 16, 0, 0);
     }
     unsigned char* Bs = As + A_BYTES;
-    const uint16_t* Wj = p.w + (int64_t)j * p.co_pad * p.ci_pad + c0;
+    const uint16_t* Wj = p.w + b * p.wsb + (int64_t)j * p.co_pad * p.ci_pad + c0;
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       const int R = (wave * B_INS + i) * RPI, row = R + lr;
@@ -681,12 +682,12 @@ extern "C" int itts_igemm_pack_dims(int Cin, int Cout, int* ci_pad, int* co_pad)
   return 0;
 }
 
-extern "C" int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, const float* bias,
-                              const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy,
-                              const int32_t* lengths, int B, int Tmax, int Cin, int Cout, int ntaps,
-                              const int32_t* tap_off, int y_row_mul, int y_row_off, float alpha, int gelu,
-                              int out_dtype, void* stream) {
-  const char* fn = "itts_igemm_fwd";
+namespace {
+int igemm_fwd_impl(const char* fn, const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, int64_t w_sb,
+                   const float* bias, const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb,
+                   int64_t ldy, const int32_t* lengths, int B, int Tmax, int Cin, int Cout, int ntaps,
+                   const int32_t* tap_off, int y_row_mul, int y_row_off, float alpha, int gelu, int out_dtype,
+                   void* stream) {
   ITTS_REQUIRE(B >= 0 && Tmax >= 0 && Cin > 0 && Cout > 0, fn, "bad sizes");
   if (B == 0 || Tmax == 0) return 0;
   ITTS_REQUIRE(ntaps >= 1 && ntaps <= kMaxTaps, fn, "ntaps must be in [1, 16]");
@@ -696,6 +697,7 @@ extern "C" int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const vo
   IgArgs a{};
   a.x = static_cast<const uint16_t*>(x);
   a.w = static_cast<const uint16_t*>(w_packed);
+  a.wsb = w_sb;
   a.bias = bias;
   a.bias_b = bias_b;
   a.r1 = r1;
@@ -729,5 +731,56 @@ extern "C" int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const vo
   hipStream_t s = itts::as_stream(stream);
   if (out_dtype == ITTS_BF16) dispatch<uint16_t>(a, vec, s);
   else dispatch<float>(a, vec, s);
+  return itts::check_launch(fn);
+}
+
+// y[m][n] = bias[n] + sum_s part[s][m][n], s ascending (fixed order: row-independent, run-to-run exact)
+__global__ __launch_bounds__(256) void splitk_sum_kernel(const float4* __restrict__ part, int nsplit, int64_t n4,
+                                                         int N4, const float4* __restrict__ bias,
+                                                         float4* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 acc = bias ? bias[i % N4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < nsplit; ++s) {
+    const float4 v = part[(int64_t)s * n4 + i];
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  y[i] = acc;
+}
+}  // namespace
+
+extern "C" int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, const float* bias,
+                              const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy,
+                              const int32_t* lengths, int B, int Tmax, int Cin, int Cout, int ntaps,
+                              const int32_t* tap_off, int y_row_mul, int y_row_off, float alpha, int gelu,
+                              int out_dtype, void* stream) {
+  return igemm_fwd_impl("itts_igemm_fwd", x, x_sb, ldx, w_packed, 0, bias, bias_b, r1, r2, y, y_sb, ldy, lengths, B,
+                        Tmax, Cin, Cout, ntaps, tap_off, y_row_mul, y_row_off, alpha, gelu, out_dtype, stream);
+}
+
+extern "C" int itts_igemm_splitk(const void* x, int64_t ldx, int M, int K, const void* w_chunks, int nsplit, int N,
+                                 const float* bias, float* partials, float* y, void* stream) {
+  const char* fn = "itts_igemm_splitk";
+  ITTS_REQUIRE(M >= 0 && K > 0 && N > 0 && nsplit >= 1 && K % nsplit == 0, fn, "bad sizes (K % nsplit == 0)");
+  ITTS_REQUIRE((K / nsplit) % 8 == 0 && N % 4 == 0 && ldx >= K, fn, "K / nsplit must be a multiple of 8, N of 4");
+  if (M == 0) return 0;
+  ITTS_REQUIRE(x && w_chunks && partials && y, fn, "null pointer");
+  ITTS_REQUIRE((reinterpret_cast<uintptr_t>(partials) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
+                   (!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0), fn, "partials, y, bias 16-byte aligned");
+  const int Kc = K / nsplit;
+  int ci_pad = 0, co_pad = 0;
+  itts_igemm_pack_dims(Kc, N, &ci_pad, &co_pad);
+  static const int32_t tap0 = 0;
+  const int rc = igemm_fwd_impl(fn, x, Kc, ldx, w_chunks, (int64_t)ci_pad * co_pad, nullptr, nullptr, nullptr, nullptr,
+                                partials, (int64_t)M * N, N, nullptr, nsplit, M, Kc, N, 1, &tap0, 1, 0, 1.0f, 0, ITTS_F32,
+                                stream);
+  if (rc) return rc;
+  const int64_t n4 = (int64_t)M * N / 4;
+  hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, itts::as_stream(stream),
+                     reinterpret_cast<const float4*>(partials), nsplit, n4, N / 4,
+                     reinterpret_cast<const float4*>(bias), reinterpret_cast<float4*>(y));
   return itts::check_launch(fn);
 }

@@ -44,6 +44,10 @@ SIGNATURES = {
                                    _c_i, _vp]),
     "itts_log_mel": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _vp, _c_i, _c_i, _c_i, _vp, _vp]),
     "itts_resample_sinc": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _c_i, _c_i, _c_i, _vp, _c_i64, _c_i, _vp]),
+    "itts_igemm_splitk": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _c_i, _c_i, _vp, _vp, _vp, _vp]),
+    "itts_cond_subsample": (_c_i, [_vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _c_i, _vp, _vp]),
+    "itts_cond_glu_dwconv": (_c_i, [_vp, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _c_i, _vp, _vp, _c_f, _vp, _c_i64, _vp,
+                                    _vp]),
     "itts_layernorm_rows": (_c_i, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp, _vp, _vp, _c_i, _vp]),
     "itts_residual_reduce_ln": (_c_i, [_vp, _c_i64, _vp, _c_i, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i, _c_i, _vp, _vp,
                                        _vp, _vp, _c_i, _vp]),

@@ -173,10 +173,19 @@ class HipGPT:
 
     # ---------------- conditioning + inputs ----------------
     @torch.no_grad()
-    def conditioning(self, mel: torch.Tensor, mel_lengths=None) -> torch.Tensor:
-        # convolutions are GEMMs (utils/convgemm.py): run-to-run identical without MIOpen
+    def conditioning(self, mel: torch.Tensor, mel_lengths=None, fast: bool = False) -> torch.Tensor:
+        """conds [B, 32, D] of prompt mels [B, 100, T].  fast=True: the linear layers on the bf16 MFMA
+        implicit GEMM (utils/hiplinear.py; the reference's fp16 mode runs this under autocast,
+        infer.py:572-586); fast=False: f32 torch (the exact-f32 verification mode and the oracle tests).
+        Convolutions are GEMMs (utils/convgemm.py): run-to-run identical without MIOpen."""
+        lin = None
+        if fast:
+            if getattr(self, "_cond_bank", None) is None:
+                from ..utils.hiplinear import HipLinearBank
+                self._cond_bank = HipLinearBank(self.sd_cond, self.dev)
+            lin = self._cond_bank
         return get_conditioning(self.sd_cond, self.cfg, mel.to(self.dev).float(),
-                                None if mel_lengths is None else mel_lengths.to(self.dev))
+                                None if mel_lengths is None else mel_lengths.to(self.dev), lin=lin)
 
     def prepare_inputs(self, conds: torch.Tensor, text_ids: torch.Tensor):
         """``prepare_gpt_inputs`` (gpt/model.py:591-654): strip ids 0/1, [0]+ids+[1], left zero pad.

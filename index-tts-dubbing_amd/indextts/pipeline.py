@@ -8,6 +8,7 @@ latent pass and the vocoder).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -62,27 +63,31 @@ class BatchedTTS:
         self.stop_text = int(cfg.gpt.stop_text_token)
         self._prompt_cache: Dict[object, tuple] = {}
         self.graph_features = True  # prompt conditioning + ECAPA replayed as a captured graph
+        # bf16 product mode: the per-prompt linear layers / 1x1 convs on the bf16 MFMA GEMM (the
+        # reference's fp16 mode autocasts them, infer.py:572-586, 613-623); f32 mode stays exact f32
+        self.fast_features = dtype == "bf16" and os.environ.get("ITTS_FAST_FEATURES", "1") != "0"
         self._feat_graphs: Dict[tuple, tuple] = {}
 
     @torch.no_grad()
     def _features(self, m: torch.Tensor):
         """conditioning latents + ECAPA speaker embedding of prompt mels m [n, 100, T]: ~300 small
         PyTorch-ROCm launches, replayed as one captured hipGraph per (n, T) after a warm-up call."""
+        fast = self.fast_features
         if not self.graph_features:
-            return self.gpt.conditioning(m), self.vocoder.speaker(m.transpose(1, 2))
-        key = tuple(m.shape)
+            return self.gpt.conditioning(m, fast=fast), self.vocoder.speaker(m.transpose(1, 2), fast=fast)
+        key = tuple(m.shape) + (fast,)
         ent = self._feat_graphs.get(key)
         if ent is None:
             static = m.clone()
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side):  # warm-up: lets the conv libraries pick their kernels
-                self.gpt.conditioning(static), self.vocoder.speaker(static.transpose(1, 2))
+                self.gpt.conditioning(static, fast=fast), self.vocoder.speaker(static.transpose(1, 2), fast=fast)
             torch.cuda.current_stream(self.device).wait_stream(side)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                c = self.gpt.conditioning(static)
-                s = self.vocoder.speaker(static.transpose(1, 2))
+                c = self.gpt.conditioning(static, fast=fast)
+                s = self.vocoder.speaker(static.transpose(1, 2), fast=fast)
             ent = self._feat_graphs[key] = (g, static, c, s)
         g, static, c, s = ent
         static.copy_(m)

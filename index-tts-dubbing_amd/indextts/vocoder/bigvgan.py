@@ -221,10 +221,18 @@ class HipBigVGAN:
 
     # ---------------- per-prompt (cached by the caller) ----------------
     @torch.no_grad()
-    def speaker(self, mel_ref: torch.Tensor) -> torch.Tensor:
+    def speaker(self, mel_ref: torch.Tensor, fast: bool = False) -> torch.Tensor:
         """mel_ref [B, T, n_mels] -> [B, spk_dim] (ECAPA; PyTorch ops on the device, convolutions as
-        im2col GEMMs: run-to-run identical without MIOpen's naive deterministic conv)."""
-        return speaker_embedding(self.sd_torch, mel_ref.to(self.device).float())
+        im2col GEMMs: run-to-run identical without MIOpen's naive deterministic conv).  fast=True: the
+        1x1 convolutions on the bf16 MFMA implicit GEMM (utils/hiplinear.py; the reference's fp16 mode
+        runs BigVGAN under autocast, infer.py:613-623)."""
+        lin = None
+        if fast:
+            if getattr(self, "_spk_bank", None) is None:
+                from ..utils.hiplinear import HipLinearBank
+                self._spk_bank = HipLinearBank(self.sd_torch, self.device)
+            lin = self._spk_bank
+        return speaker_embedding(self.sd_torch, mel_ref.to(self.device).float(), lin=lin)
 
     @torch.no_grad()
     def cond_biases(self, spk: torch.Tensor):

@@ -1,4 +1,4 @@
-"""mlp.c_proj of the decode step (B = 32, K = 4096, N = 1024, bf16 weights from HBM, rotating copies):
+"""EXPERIMENT (itts_decode_gemm_reduce removed after measurement; it lives in commit 1e98b38). mlp.c_proj of the decode step (B = 32, K = 4096, N = 1024, bf16 weights from HBM, rotating copies):
 split-K 8 partials + the residual reduce launch (itts_decode_gemm epi 2 + itts_residual_reduce_ln)
 vs split-K with the last-arriver reduce inside the launch (itts_decode_gemm_reduce).  Checks x / xh
 bit-identical between the two and the tile counters left at zero."""

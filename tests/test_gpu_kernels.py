@@ -376,3 +376,58 @@ def test_resample_kernel_matches_cpu_front_end(orig):
     got = resample_hip(x.cuda(), orig, 24000).cpu()
     assert got.shape == want.shape
     assert float((got - want).abs().max()) <= 2e-6
+
+
+@pytest.mark.parametrize("C,T", [(512, 511), (64, 40), (32, 7)])
+def test_cond_subsample_matches_conv2d(C, T):
+    """itts_cond_subsample vs F.conv2d(stride 2) + ReLU (Conv2dSubsampling2) in f32, read back in
+    (t, f, c) order: |err| <= bf16 output rounding (2^-8 relative) + 1e-5."""
+    from indextts.utils.hiplinear import HipLinearBank
+    g = torch.Generator().manual_seed(C + T)
+    mel = torch.randn(3, 100, T, generator=g) * 2 - 4
+    sd = {"e.conv.0.weight": torch.randn(C, 1, 3, 3, generator=g) * 0.3, "e.conv.0.bias": torch.randn(C, generator=g)}
+    bank = HipLinearBank({k: v.cuda() for k, v in sd.items()}, "cuda")
+    got = bank.subsample(mel.cuda(), "e").float().cpu()
+    want = F.relu(F.conv2d(mel.transpose(1, 2)[:, None], sd["e.conv.0.weight"], sd["e.conv.0.bias"], stride=2))
+    want = want.permute(0, 2, 3, 1).reshape(3, want.shape[2], -1)  # [B, t, f * C] in (f, c) order
+    assert got.shape == want.shape
+    assert float(((got - want).abs() - want.abs() * 2 ** -8).max()) <= 1e-5
+
+
+@pytest.mark.parametrize("C,T,K", [(512, 255, 15), (64, 9, 15), (36, 20, 5), (256, 37, 15), (768, 20, 7), (512, 5, 15)])
+def test_cond_glu_dwconv_matches_torch(C, T, K):
+    """itts_cond_glu_dwconv vs F.glu -> depthwise F.conv1d(padding K/2) -> LayerNorm -> SiLU in f32:
+    |err| <= 1e-4 + bf16 output rounding."""
+    from indextts.utils.hiplinear import HipLinearBank
+    g = torch.Generator().manual_seed(C + T + K)
+    a = torch.randn(2, T, 2 * C, generator=g)
+    sd = {"m.depthwise_conv.weight": torch.randn(C, 1, K, generator=g) * 0.3,
+          "m.depthwise_conv.bias": torch.randn(C, generator=g) * 0.1,
+          "m.norm.weight": 1 + 0.1 * torch.randn(C, generator=g), "m.norm.bias": 0.1 * torch.randn(C, generator=g)}
+    bank = HipLinearBank({k: v.cuda() for k, v in sd.items()}, "cuda")
+    got = bank.glu_dwconv(a.cuda(), "m").float().cpu()
+    bank.tiled = False
+    assert float((bank.glu_dwconv(a.cuda(), "m").float().cpu() - got).abs().max()) <= 2e-2
+    h = F.glu(a, dim=-1).transpose(1, 2)
+    h = F.conv1d(h, sd["m.depthwise_conv.weight"], sd["m.depthwise_conv.bias"], padding=K // 2, groups=C)
+    want = F.silu(F.layer_norm(h.transpose(1, 2), (C,), sd["m.norm.weight"], sd["m.norm.bias"], 1e-5))
+    assert float(((got - want).abs() - want.abs() * 2 ** -8).max()) <= 1e-4
+
+
+@pytest.mark.parametrize("M,K,N", [(8160, 25088, 512), (300, 4096, 96), (40, 2048, 512)])
+def test_igemm_splitk_matches_linear(M, K, N):
+    """itts_igemm_splitk (K in chunks as a batch of 1-tap GEMMs + fixed-order sum) vs F.linear on the
+    bf16-rounded operands in f32: |err| <= 1e-4 * (|A| @ |W|^T) + 1e-5; equals the unsplit bank call
+    within the same bound."""
+    from indextts.utils.hiplinear import HipLinearBank
+    g = torch.Generator().manual_seed(M + K)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g) * 0.1
+    x = torch.randn(M, K, generator=g)
+    bank = HipLinearBank({"l.weight": w.cuda(), "l.bias": b.cuda()}, "cuda")
+    got = bank.splitk(x.cuda(), "l").cpu()
+    xq, wq = x.to(torch.bfloat16).float(), w.to(torch.bfloat16).float()
+    want = F.linear(xq, wq, b)
+    bound = 1e-4 * (xq.abs() @ wq.abs().t()) + 1e-5
+    assert bool(((got - want).abs() <= bound).all()), float((got - want).abs().max())
+    assert bool(((bank(x.cuda(), "l").cpu() - got).abs() <= bound).all())
