@@ -67,6 +67,7 @@ int itts_igemm_pack_dims(int Cin, int Cout, int* ci_pad, int* co_pad);
  * AMPBlock1 dilated convs with the residual add and the /num_kernels average fused in,
  * models.py:65-74,224-243), the polyphase ConvTranspose1d upsamplers (models.py:155-161,228-231)
  * and the GPT sequence GEMMs (HF Conv1D, pytorch_utils.py:119, as 1-tap convolutions).
+ * act: gelu = 1 -> gelu_tanh, 2 -> SiLU (the conditioning encoder's feed-forward).
  * tap_off is a HOST array of ntaps offsets. */
 int itts_igemm_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, const float* bias,
                    const float* bias_b, const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy,
@@ -166,6 +167,22 @@ int itts_resample_sinc(const float* x, int64_t ldx, int B, int L, const float* k
  * (pointwise_conv1 output, 2C channels) -> GLU -> depthwise conv1d w [C][K] (+w_bias, zero padding K/2)
  * -> LayerNorm(ln_g, ln_b, eps) -> SiLU -> bf16 y [B][T][ldy].  w_t (optional, 16-B aligned): w transposed
  * [K][C], enables the LDS-tiled form for C = 256, 512 or 1024. */
+/* ECAPA speaker encoder, bf16 product path (channel-last, vocoder/ecapa.py speaker_embedding_cl):
+ * itts_pad_rows_bf16 -- y bf16 [B][T + 2 pad][Cp] = x (+ x2, optional) rows, reflect (speechbrain "same"
+ * padding, nnet/CNN.py:411-488) or zero padded in time, channels [C, Cp) zero; x / x2 f32 with batch and row
+ * strides.  itts_relu_affine_rows -- y = relu(x) * scale + shift per channel (TDNNBlock's ReLU + eval
+ * BatchNorm1d folded, BigVGAN/ECAPA_TDNN.py TDNNBlock), y may alias x. */
+int itts_pad_rows_bf16(const float* x, int64_t x_sb, int64_t ldx, const float* x2, int64_t x2_sb, int64_t ldx2, int B,
+                       int T, int C, int pad, int reflect, int Cp, void* y, void* stream);
+int itts_relu_affine_rows(const float* x, int64_t x_sb, int64_t ldx, int B, int T, int C, const float* scale,
+                          const float* shift, float* y, int64_t y_sb, int64_t ldy, void* stream);
+/* itts_cond_rel_attn -- RelPositionMultiHeadedAttention (gpt/conformer/attention.py:235-312, no rel_shift),
+ * head dim 64, H heads (C = 64 H): qkv f32 [B][T][ld_qkv] = (q | k | v) linear outputs, pos f32 [T][ld_pos]
+ * = linear_pos(pos_emb), bias_u / bias_v [H][64]; score = ((q+u).k + (q+v).p) * scale over keys t < lens[b]
+ * (lens may be null = T; an all-masked row gives 0), softmax, @ v -> out [B][T][ld_out] (f32 or bf16). */
+int itts_cond_rel_attn(const float* qkv, int64_t ld_qkv, const float* pos, int64_t ld_pos, const float* bias_u,
+                       const float* bias_v, const int32_t* lens, int B, int T, int H, float scale, void* out,
+                       int64_t ld_out, int out_dtype, void* stream);
 int itts_cond_subsample(const float* mel, int64_t mel_sb, int64_t mel_ld, int B, int n_bins, int T, const float* w,
                         const float* bias, int C, void* y, void* stream);
 int itts_cond_glu_dwconv(const float* a, int64_t lda, int B, int T, int C, const float* w, const float* w_bias, int K,

@@ -190,7 +190,211 @@ __global__ __launch_bounds__(256) void glu_dwconv_tiled_kernel(const float* __re
   }
 }
 
+// RelPositionMultiHeadedAttention (gpt/conformer/attention.py:235-312, no rel_shift) for head dim 64:
+// score(i, j) = ((q_i + u) . k_j + (q_i + v) . p_j) * scale over keys j < len (others excluded, an
+// all-masked row gives 0 -- the reference's masked_fill(-inf) / softmax / masked_fill(0)), softmax,
+// @ v.  A workgroup takes 32 query steps of one (row, head): the 128-wide concatenations (q+u | q+v)
+// and (k | p) make the two products one dot product; keys in tiles of 64 through LDS with an online
+// softmax.  f32 FMA throughout, fixed order: a row's result does not depend on the batch.
+template <typename OutT>
+__global__ __launch_bounds__(256) void rel_attn_kernel(const float* __restrict__ qkv, int64_t ldq,
+                                                       const float* __restrict__ pos, int64_t ldp,
+                                                       const float* __restrict__ bu, const float* __restrict__ bv,
+                                                       const int32_t* __restrict__ lens, int T, int H, float scale,
+                                                       OutT* __restrict__ out, int64_t ldo) {
+  // row pitches padded to 4 mod 32 words: the 8 keys / rows a wave reads with 16-B loads hit distinct banks
+  constexpr int DK = 64, QR = 32, KT = 64, QP = 2 * DK + 4, VP = DK + 4, PP = KT + 4;
+  __shared__ __attribute__((aligned(16))) float qs[QR * QP];
+  __shared__ __attribute__((aligned(16))) float ks[KT * QP];
+  __shared__ __attribute__((aligned(16))) float vs[KT * VP];
+  __shared__ __attribute__((aligned(16))) float ps[QR * PP];
+  const int i0 = blockIdx.x * QR, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+  const int C = H * DK, len = lens ? min(lens[b], T) : T;
+  const float* base = qkv + (int64_t)b * T * ldq;
+  for (int e = tid; e < QR * DK / 4; e += 256) {
+    const int r = e / (DK / 4), d = (e - r * (DK / 4)) * 4, t = i0 + r;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < T) q = *reinterpret_cast<const float4*>(base + (int64_t)t * ldq + h * DK + d);
+    const float4 u = *reinterpret_cast<const float4*>(bu + h * DK + d);
+    const float4 v = *reinterpret_cast<const float4*>(bv + h * DK + d);
+    *reinterpret_cast<float4*>(qs + r * QP + d) = make_float4(q.x + u.x, q.y + u.y, q.z + u.z, q.w + u.w);
+    *reinterpret_cast<float4*>(qs + r * QP + DK + d) = make_float4(q.x + v.x, q.y + v.y, q.z + v.z, q.w + v.w);
+  }
+  const int r = tid >> 3, g = tid & 7;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float mrun = -INFINITY, lrun = 0.f;
+  for (int k0 = 0; k0 < len; k0 += KT) {
+    __syncthreads();  // previous tile fully consumed (and qs written)
+    for (int e = tid; e < KT * DK / 4; e += 256) {
+      const int j = e / (DK / 4), d = (e - j * (DK / 4)) * 4, t = k0 + j;
+      float4 kk = make_float4(0.f, 0.f, 0.f, 0.f), pp = kk, vv = kk;
+      if (t < len) {
+        const float* row = base + (int64_t)t * ldq;
+        kk = *reinterpret_cast<const float4*>(row + C + h * DK + d);
+        vv = *reinterpret_cast<const float4*>(row + 2 * C + h * DK + d);
+        pp = *reinterpret_cast<const float4*>(pos + (int64_t)t * ldp + h * DK + d);
+      }
+      *reinterpret_cast<float4*>(ks + j * QP + d) = kk;
+      *reinterpret_cast<float4*>(ks + j * QP + DK + d) = pp;
+      *reinterpret_cast<float4*>(vs + j * VP + d) = vv;
+    }
+    __syncthreads();
+    float sc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int d = 0; d < 2 * DK; d += 4) {  // 8 independent dot products, 16-B LDS reads
+      const float4 q = *reinterpret_cast<const float4*>(qs + r * QP + d);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const float4 kv = *reinterpret_cast<const float4*>(ks + (g + 8 * m) * QP + d);
+        sc[m] = fmaf(q.x, kv.x, sc[m]);
+        sc[m] = fmaf(q.y, kv.y, sc[m]);
+        sc[m] = fmaf(q.z, kv.z, sc[m]);
+        sc[m] = fmaf(q.w, kv.w, sc[m]);
+      }
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      sc[m] = (k0 + g + 8 * m < len) ? sc[m] * scale : -INFINITY;
+      tmax = fmaxf(tmax, sc[m]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 1, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 2, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 4, 64));
+    const float mnew = fmaxf(mrun, tmax);  // finite: key k0 < len is valid
+    const float corr = __expf(mrun - mnew);
+    float psum = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float pe = sc[m] == -INFINITY ? 0.f : __expf(sc[m] - mnew);
+      ps[r * PP + g + 8 * m] = pe;
+      psum += pe;
+    }
+    psum += __shfl_xor(psum, 1, 64);
+    psum += __shfl_xor(psum, 2, 64);
+    psum += __shfl_xor(psum, 4, 64);
+    lrun = lrun * corr + psum;
+    mrun = mnew;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] *= corr;
+    __syncthreads();
+    for (int j = 0; j < KT; j += 4) {
+      const float4 pe = *reinterpret_cast<const float4*>(ps + r * PP + j);
+      const float pj[4] = {pe.x, pe.y, pe.z, pe.w};
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float4 v0 = *reinterpret_cast<const float4*>(vs + (j + jj) * VP + g * 8);
+        const float4 v1 = *reinterpret_cast<const float4*>(vs + (j + jj) * VP + g * 8 + 4);
+        acc[0] = fmaf(pj[jj], v0.x, acc[0]);
+        acc[1] = fmaf(pj[jj], v0.y, acc[1]);
+        acc[2] = fmaf(pj[jj], v0.z, acc[2]);
+        acc[3] = fmaf(pj[jj], v0.w, acc[3]);
+        acc[4] = fmaf(pj[jj], v1.x, acc[4]);
+        acc[5] = fmaf(pj[jj], v1.y, acc[5]);
+        acc[6] = fmaf(pj[jj], v1.z, acc[6]);
+        acc[7] = fmaf(pj[jj], v1.w, acc[7]);
+      }
+    }
+  }
+  const int t = i0 + r;
+  if (t >= T) return;
+  const float inv = lrun > 0.f ? 1.f / lrun : 0.f;
+  OutT* o = out + ((int64_t)b * T + t) * ldo + h * DK + g * 8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) St<OutT>::st(o + i, acc[i] * inv);
+}
+
+// ECAPA (channel-last product path): y[b][tp][c] = bf16(x[b][src(tp)][c] (+ x2[b][src(tp)][c])) for
+// tp < T + 2 pad, src reflecting at the ends (speechbrain "same" reflect padding) or zero padding;
+// channels [C, Cp) zero (pads Cin to a multiple of 8 for the 16-B igemm loads).  4 channels per thread.
+__global__ __launch_bounds__(256) void pad_rows_kernel(const float* __restrict__ x, int64_t x_sb, int64_t ldx,
+                                                       const float* __restrict__ x2, int64_t x2_sb, int64_t ldx2,
+                                                       int T, int C, int pad, int reflect, int Cp,
+                                                       uint16_t* __restrict__ y) {
+  const int Tp = T + 2 * pad, b = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (tp, c4)
+  const int cq = Cp / 4;
+  if (i >= (int64_t)Tp * cq) return;
+  const int tp = (int)(i / cq), c = (int)(i - (int64_t)tp * cq) * 4;
+  int t = tp - pad;
+  bool ok = true;
+  if (t < 0 || t >= T) {
+    if (reflect) t = t < 0 ? -t : 2 * (T - 1) - t;
+    else ok = false;
+  }
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k < C) {
+        v[k] = x[(int64_t)b * x_sb + (int64_t)t * ldx + c + k];
+        if (x2) v[k] += x2[(int64_t)b * x2_sb + (int64_t)t * ldx2 + c + k];
+      }
+  }
+  *reinterpret_cast<uint2*>(y + ((int64_t)b * Tp + tp) * Cp + c) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+}
+
+// y = relu(x) * scale[c] + shift[c] (TDNNBlock: BatchNorm1d(eval) after ReLU, folded to an affine map)
+__global__ __launch_bounds__(256) void relu_affine_kernel(const float* __restrict__ x, int64_t x_sb, int64_t ldx, int T,
+                                                          int C, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float* __restrict__ y,
+                                                          int64_t y_sb, int64_t ldy) {
+  const int b = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)T * C) return;
+  const int t = (int)(i / C), c = (int)(i - (int64_t)t * C);
+  const float v = x[(int64_t)b * x_sb + (int64_t)t * ldx + c];
+  y[(int64_t)b * y_sb + (int64_t)t * ldy + c] = fmaf(fmaxf(v, 0.f), scale[c], shift[c]);
+}
+
 }  // namespace
+
+extern "C" int itts_pad_rows_bf16(const float* x, int64_t x_sb, int64_t ldx, const float* x2, int64_t x2_sb,
+                                  int64_t ldx2, int B, int T, int C, int pad, int reflect, int Cp, void* y,
+                                  void* stream) {
+  const char* fn = "itts_pad_rows_bf16";
+  ITTS_REQUIRE(B >= 0 && T >= 0 && C > 0 && pad >= 0 && Cp >= C && Cp % 4 == 0, fn, "bad sizes (Cp >= C, Cp % 4 == 0)");
+  ITTS_REQUIRE(!reflect || pad < T, fn, "reflect padding needs pad < T");
+  if (B == 0 || T == 0) return 0;
+  ITTS_REQUIRE(x && y && (reinterpret_cast<uintptr_t>(y) & 7) == 0, fn, "null pointer or y not 8-byte aligned");
+  const int64_t n = (int64_t)(T + 2 * pad) * (Cp / 4);
+  hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)((n + 255) / 256), B), dim3(256), 0, itts::as_stream(stream), x,
+                     x_sb, ldx, x2, x2_sb, ldx2, T, C, pad, reflect, Cp, static_cast<uint16_t*>(y));
+  return itts::check_launch(fn);
+}
+
+extern "C" int itts_relu_affine_rows(const float* x, int64_t x_sb, int64_t ldx, int B, int T, int C, const float* scale,
+                                     const float* shift, float* y, int64_t y_sb, int64_t ldy, void* stream) {
+  const char* fn = "itts_relu_affine_rows";
+  ITTS_REQUIRE(B >= 0 && T >= 0 && C > 0, fn, "bad sizes");
+  if (B == 0 || T == 0) return 0;
+  ITTS_REQUIRE(x && scale && shift && y, fn, "null pointer");
+  const int64_t n = (int64_t)T * C;
+  hipLaunchKernelGGL(relu_affine_kernel, dim3((unsigned)((n + 255) / 256), B), dim3(256), 0, itts::as_stream(stream),
+                     x, x_sb, ldx, T, C, scale, shift, y, y_sb, ldy);
+  return itts::check_launch(fn);
+}
+
+extern "C" int itts_cond_rel_attn(const float* qkv, int64_t ld_qkv, const float* pos, int64_t ld_pos,
+                                  const float* bias_u, const float* bias_v, const int32_t* lens, int B, int T, int H,
+                                  float scale, void* out, int64_t ld_out, int out_dtype, void* stream) {
+  const char* fn = "itts_cond_rel_attn";
+  ITTS_REQUIRE(B >= 0 && T >= 0 && H > 0, fn, "bad sizes");
+  ITTS_REQUIRE(ld_qkv >= 3 * 64 * H && ld_pos >= 64 * H && ld_out >= 64 * H, fn, "head dim 64: ld_qkv >= 3C, ld_out >= C");
+  ITTS_REQUIRE(out_dtype == ITTS_F32 || out_dtype == ITTS_BF16, fn, "out dtype f32 (0) or bf16 (1)");
+  if (B == 0 || T == 0) return 0;
+  ITTS_REQUIRE(qkv && pos && bias_u && bias_v && out, fn, "null pointer");
+  ITTS_REQUIRE(ld_qkv % 4 == 0 && ld_pos % 4 == 0 && ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(pos) |
+                reinterpret_cast<uintptr_t>(bias_u) | reinterpret_cast<uintptr_t>(bias_v)) & 15) == 0,
+               fn, "qkv, pos, biases 16-byte aligned with row pitches a multiple of 4");
+  dim3 grid((T + 31) / 32, H, B);
+  if (out_dtype == ITTS_BF16)
+    hipLaunchKernelGGL(rel_attn_kernel<uint16_t>, grid, dim3(256), 0, itts::as_stream(stream), qkv, ld_qkv, pos, ld_pos,
+                       bias_u, bias_v, lens, T, H, scale, static_cast<uint16_t*>(out), ld_out);
+  else
+    hipLaunchKernelGGL(rel_attn_kernel<float>, grid, dim3(256), 0, itts::as_stream(stream), qkv, ld_qkv, pos, ld_pos,
+                       bias_u, bias_v, lens, T, H, scale, static_cast<float*>(out), ld_out);
+  return itts::check_launch(fn);
+}
 
 extern "C" int itts_cond_subsample(const float* mel, int64_t mel_sb, int64_t mel_ld, int B, int n_bins, int T,
                                    const float* w, const float* bias, int C, void* y, void* stream) {

@@ -9,7 +9,7 @@
 // exact).  Layout is channel-last: X [B][Tmax][ldx] bf16, Y [B][Tout][ldy] (bf16 or f32).
 // Wp is prepacked on the host: [ntaps][co_pad][ci_pad] bf16, zero padded.
 //
-// Epilogue: v = acc + bias[n] + bias_b[b][n]; if gelu: v = gelu_tanh(v); v = alpha*(v + r1 + r2)
+// Epilogue: v = acc + bias[n] + bias_b[b][n]; gelu 1: v = gelu_tanh(v), 2: v = silu(v); v = alpha*(v + r1 + r2)
 // (r1/r2 residual tensors with Y's layout and dtype; r1 may alias Y).
 //
 // Tiling: one wave per WM x WN sub-tile of the TM x TN block tile, K step KC (channels of one tap) staged
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(64 * (TM / WM) * (TN / WN)) void igemm_kernel(IgArg
         if (q >= len) continue;
         const int64_t off = (int64_t)(q * p.ymul + p.yoff) * p.ldy + n;
         float v = acc[i][j][r] + bn;
-        if (p.gelu) v = gelu_tanh(v);
+        if (p.gelu) v = p.gelu == 2 ? v / (1.f + __expf(-v)) : gelu_tanh(v);
         if (R1) v += St<OutT>::ld(R1 + off);
         if (R2) v += St<OutT>::ld(R2 + off);
         St<OutT>::st(Y + off, p.alpha * v);
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float v = acc[i][j][r] + bn[j];
-        if (p.gelu) v = gelu_tanh(v);
+        if (p.gelu) v = p.gelu == 2 ? v / (1.f + __expf(-v)) : gelu_tanh(v);
         stg[((r & 3) + 8 * (r >> 2) + 4 * h) * EP + 32 * j + r32] = v;
       }
 #pragma unroll

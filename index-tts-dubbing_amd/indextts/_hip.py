@@ -45,6 +45,11 @@ SIGNATURES = {
     "itts_log_mel": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _vp, _c_i, _c_i, _c_i, _vp, _vp]),
     "itts_resample_sinc": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _c_i, _c_i, _c_i, _vp, _c_i64, _c_i, _vp]),
     "itts_igemm_splitk": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _c_i, _c_i, _vp, _vp, _vp, _vp]),
+    "itts_pad_rows_bf16": (_c_i, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_i, _c_i, _c_i, _vp,
+                                  _vp]),
+    "itts_relu_affine_rows": (_c_i, [_vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _vp, _c_i64, _c_i64, _vp]),
+    "itts_cond_rel_attn": (_c_i, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_f, _vp, _c_i64, _c_i,
+                                  _vp]),
     "itts_cond_subsample": (_c_i, [_vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _c_i, _vp, _vp]),
     "itts_cond_glu_dwconv": (_c_i, [_vp, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _c_i, _vp, _vp, _c_f, _vp, _c_i64, _vp,
                                     _vp]),

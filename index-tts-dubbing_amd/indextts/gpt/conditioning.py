@@ -39,6 +39,8 @@ def _ln(x, sd, name, eps=1e-5):
 
 
 def _rel_pos_mha(x, sd, p, heads, mask, pos_emb, lin=None):
+    if lin is not None:  # fused qkv GEMM + HIP attention (csrc/cond_ops.hip), bf16 into linear_out
+        return lin.rel_attn(x, p, heads, mask, pos_emb)
     B, T, C = x.shape
     dk = C // heads
     q = _lin(x, sd, p + ".linear_q", lin=lin).view(B, T, heads, dk)
@@ -55,11 +57,15 @@ def _rel_pos_mha(x, sd, p, heads, mask, pos_emb, lin=None):
     return _lin(out, sd, p + ".linear_out", lin=lin)
 
 
-def _conv_module(x, sd, p, mask, lin=None):
+def _conv_module(x, sd, p, mask, lin=None, residual=None):
+    """residual (fast path, all frames valid): pointwise_conv2 adds into it in place, returns None."""
     C = x.shape[-1]
     if lin is not None:  # channel-last: the pointwise convs are linear layers over the rows
-        h = x.masked_fill(~mask.transpose(1, 2), 0.0)
+        h = x if residual is not None else x.masked_fill(~mask.transpose(1, 2), 0.0)
         h = lin.glu_dwconv(lin(h, p + ".pointwise_conv1"), p)  # GLU, depthwise, LN, SiLU fused (bf16 out)
+        if residual is not None:
+            lin(h, p + ".pointwise_conv2", out=residual, residual=residual)
+            return None
         return lin(h, p + ".pointwise_conv2").masked_fill(~mask.transpose(1, 2), 0.0)
     h = x.transpose(1, 2).masked_fill(~mask, 0.0)  # [B, C, T]
     h = conv1d(h, sd[p + ".pointwise_conv1.weight"], sd[p + ".pointwise_conv1.bias"])
@@ -71,8 +77,9 @@ def _conv_module(x, sd, p, mask, lin=None):
     return h.masked_fill(~mask, 0.0).transpose(1, 2)
 
 
-def conformer_encode(sd, mel, mel_lengths, heads: int, num_blocks: int, prefix="conditioning_encoder", lin=None):
-    """mel [B, n_mels, T] -> (xs [B, T', C], mask [B, 1, T'])."""
+def conformer_encode(sd, mel, mel_lengths, heads: int, num_blocks: int, prefix="conditioning_encoder", lin=None,
+                     full=False):
+    """mel [B, n_mels, T] -> (xs [B, T', C], mask [B, 1, T']).  full: every frame valid (host-known)."""
     x = mel.transpose(1, 2)
     B, T, _ = x.shape
     valid = torch.arange(T, device=x.device)[None, :] < mel_lengths.to(x.device)[:, None]
@@ -91,6 +98,15 @@ def conformer_encode(sd, mel, mel_lengths, heads: int, num_blocks: int, prefix="
     mask = mask[:, :, 2::2]
     for i in range(num_blocks):
         q = f"{prefix}.encoders.{i}"
+        if lin is not None:  # LN -> bf16 operands, residual adds and SiLU in the GEMM epilogues
+            lin.rel_attn(lin.ln(h, q + ".norm_mha"), q + ".self_attn", heads, mask, pos_emb, residual=h)
+            c = _conv_module(lin.ln(h, q + ".norm_conv"), sd, q + ".conv_module", mask, lin, residual=h if full else None)
+            if c is not None:
+                h = h + c
+            f = lin(lin.ln(h, q + ".norm_ff"), q + ".feed_forward.w_1", act=2, bf16_out=True)
+            lin(f, q + ".feed_forward.w_2", out=h, residual=h)
+            h = _ln(h, sd, q + ".norm_final")
+            continue
         h = h + _rel_pos_mha(_ln(h, sd, q + ".norm_mha"), sd, q + ".self_attn", heads, mask, pos_emb, lin)
         h = h + _conv_module(_ln(h, sd, q + ".norm_conv"), sd, q + ".conv_module", mask, lin)
         y = _ln(h, sd, q + ".norm_ff")
@@ -134,9 +150,11 @@ def get_conditioning(sd, cfg_gpt, mel, mel_lengths=None, lin=None):
     product mode (utils/hiplinear.HipLinearBank); None = f32 torch (verification mode, oracle tests)."""
     if mel.ndim == 2:
         mel = mel.unsqueeze(0)
+    full = mel_lengths is None  # every frame valid: known on the host (no mask work, fused residuals)
     if mel_lengths is None:
         mel_lengths = torch.full((mel.shape[0],), mel.shape[-1], dtype=torch.long, device=mel.device)
     cm = cfg_gpt.condition_module
-    xs, mask = conformer_encode(sd, mel, mel_lengths, int(cm.attention_heads), int(cm.num_blocks), lin=lin)
+    xs, mask = conformer_encode(sd, mel, mel_lengths, int(cm.attention_heads), int(cm.num_blocks), lin=lin,
+                                full=full)
     key_mask = F.pad(mask.squeeze(1), (32, 0), value=True)
     return perceiver_resample(sd, xs, key_mask, int(cm.attention_heads), lin=lin)

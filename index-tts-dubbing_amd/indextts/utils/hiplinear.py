@@ -52,8 +52,10 @@ class HipLinearBank:
             self._packed[name] = ent
         return ent
 
-    def __call__(self, x: torch.Tensor, name: str, bias: bool = True,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, name: str, bias: bool = True, out: Optional[torch.Tensor] = None,
+                 act: int = 0, bf16_out: bool = False, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """y = act(x @ W^T + b) (+ residual); act 1 = gelu_tanh, 2 = SiLU; bf16_out: bf16 y (the next
+        GEMM's operand); residual (f32, contiguous, may be ``out`` itself: y += in place)."""
         wp, b, N, K = self._pack(name)
         assert x.shape[-1] == K, (name, x.shape, K)
         lead = x.shape[:-1]
@@ -61,12 +63,30 @@ class HipLinearBank:
         if K % 8 or a.stride(0) != K:
             a = a.contiguous()
         M = a.shape[0]
-        y = torch.empty(M, N, dtype=torch.float32, device=self.dev) if out is None else out.view(M, N)
+        dt = torch.bfloat16 if bf16_out else torch.float32
+        y = torch.empty(M, N, dtype=dt, device=self.dev) if out is None else out.view(M, N)
+        assert y.dtype == dt and y.is_contiguous()
+        r = None
+        if residual is not None:
+            r = residual.view(M, N)
+            assert r.dtype == torch.float32 and r.is_contiguous() and not bf16_out
         _hip.check(self.lib.itts_igemm_fwd(
-            a.data_ptr(), M * K, K, wp.data_ptr(), _hip.ptr(b if bias else None), None, None, None, y.data_ptr(),
-            M * N, N, None, 1, M, K, N, 1, _hip.i32_array([0]), 1, 0, 1.0, 0, _hip.F32, _hip.stream_ptr(self.dev)),
-            "itts_igemm_fwd")
+            a.data_ptr(), M * K, K, wp.data_ptr(), _hip.ptr(b if bias else None), None, _hip.ptr(r), None,
+            y.data_ptr(), M * N, N, None, 1, M, K, N, 1, _hip.i32_array([0]), 1, 0, 1.0, act,
+            _hip.BF16 if bf16_out else _hip.F32, _hip.stream_ptr(self.dev)), "itts_igemm_fwd")
         return y.view(*lead, N)
+
+    def ln(self, x: torch.Tensor, name: str) -> torch.Tensor:
+        """LayerNorm(eps 1e-5) of the rows of x [..., D] f32 -> bf16 (the next GEMM's operand), one
+        kernel (itts_layernorm_rows) instead of LayerNorm + cast."""
+        D = x.shape[-1]
+        xr = x.reshape(-1, D)
+        assert xr.stride(1) == 1
+        y = torch.empty(xr.shape[0], D, dtype=torch.bfloat16, device=self.dev)
+        _hip.check(self.lib.itts_layernorm_rows(xr.data_ptr(), xr.stride(0), None, y.data_ptr(), D, xr.shape[0], D,
+                                                self.sd[name + ".weight"].data_ptr(), self.sd[name + ".bias"].data_ptr(),
+                                                None, None, _hip.BF16, _hip.stream_ptr(self.dev)), "itts_layernorm_rows")
+        return y.view(*x.shape)
 
     def subsample(self, mel: torch.Tensor, name: str) -> torch.Tensor:
         """``relu(conv2d(mel^T[:, None], stride 2))`` of Conv2dSubsampling2 (gpt/conformer/subsampling.py:
@@ -149,3 +169,91 @@ class HipLinearBank:
             self.sd[name + ".norm.bias"].float().contiguous().data_ptr(), eps, y.data_ptr(), C,
             _hip.ptr(self.sd[key] if self.tiled else None), _hip.stream_ptr(self.dev)), "itts_cond_glu_dwconv")
         return y
+
+    def rel_attn(self, x: torch.Tensor, name: str, heads: int, mask: torch.Tensor, pos_emb: torch.Tensor,
+                 residual: Optional[torch.Tensor] = None):
+        """RelPositionMultiHeadedAttention (gpt/conformer/attention.py:235-312) of x [B, T, C] f32 with
+        key mask [B, 1, T] (a valid prefix per row): q/k/v as one fused GEMM, the attention in
+        ``itts_cond_rel_attn`` (row-independent), linear_out on its bf16 output."""
+        B, T, C = x.shape
+        key = name + ".linear_qkv"
+        if key + ".weight" not in self.sd:
+            self.register(key, torch.cat([self.sd[f"{name}.linear_{c}.weight"] for c in "qkv"], 0).contiguous(),
+                          torch.cat([self.sd[f"{name}.linear_{c}.bias"] for c in "qkv"], 0).contiguous())
+        assert C == 64 * heads, "head dim 64"
+        qkv = self(x, key)
+        pos = torch.nn.functional.linear(pos_emb[0], self.sd[name + ".linear_pos.weight"]).contiguous()
+        lens = mask.reshape(B, -1).sum(-1, dtype=torch.int32)
+        out = torch.empty(B, T, C, dtype=torch.bfloat16, device=self.dev)
+        _hip.check(self.lib.itts_cond_rel_attn(
+            qkv.data_ptr(), 3 * C, pos.data_ptr(), C, self.sd[name + ".pos_bias_u"].contiguous().data_ptr(),
+            self.sd[name + ".pos_bias_v"].contiguous().data_ptr(), lens.data_ptr(), B, T, heads, 1.0 / 8.0,
+            out.data_ptr(), C, _hip.BF16, _hip.stream_ptr(self.dev)), "itts_cond_rel_attn")
+        return self(out, name + ".linear_out", out=residual, residual=residual)
+
+    # ---------------- ECAPA channel-last (vocoder/ecapa.py speaker_embedding_cl) ----------------
+    def pad_rows(self, x: torch.Tensor, pad: int, reflect: bool = True, x2: Optional[torch.Tensor] = None,
+                 cp: Optional[int] = None) -> torch.Tensor:
+        """bf16 [B, T + 2 pad, cp] of the f32 rows x (+ x2) [B, T, C] (unit channel stride), reflect or
+        zero padded in time, channels beyond C zero."""
+        B, T, C = x.shape
+        cp = cp or (C + 7) // 8 * 8
+        assert x.stride(2) == 1 and (x2 is None or (x2.shape == x.shape and x2.stride(2) == 1))
+        y = torch.empty(B, T + 2 * pad, cp, dtype=torch.bfloat16, device=self.dev)
+        _hip.check(self.lib.itts_pad_rows_bf16(
+            x.data_ptr(), x.stride(0), x.stride(1), _hip.ptr(x2), 0 if x2 is None else x2.stride(0),
+            0 if x2 is None else x2.stride(1), B, T, C, pad, 1 if reflect else 0, cp, y.data_ptr(),
+            _hip.stream_ptr(self.dev)), "itts_pad_rows_bf16")
+        return y
+
+    def conv_taps(self, xp: torch.Tensor, name: str, dilation: int, out: Optional[torch.Tensor] = None):
+        """conv1d (weight [Cout, Cin, k], bias) over the padded bf16 rows xp [B, Tp, Cp] -> f32
+        [B, Tp, Cout]; rows [0, Tp - dilation (k - 1)) are the valid ("same") outputs."""
+        B, Tp, Cp = xp.shape
+        key = ("taps", name)
+        ent = self._packed.get(key)
+        if ent is None:
+            from ..vocoder.bigvgan import pack_taps
+            w = self.sd[name + ".weight"].float().cpu()
+            co, ci, k = w.shape
+            wp = torch.zeros(co, Cp, k)
+            wp[:, :ci] = w
+            ent = self._packed[key] = (pack_taps([wp[:, :, j].contiguous() for j in range(k)], Cp, co).to(self.dev),
+                                       self.sd[name + ".bias"].float().contiguous().to(self.dev), co, k)
+        wpk, b, co, k = ent
+        y = torch.empty(B, Tp, co, dtype=torch.float32, device=self.dev) if out is None else out
+        _hip.check(self.lib.itts_igemm_fwd(
+            xp.data_ptr(), Tp * Cp, Cp, wpk.data_ptr(), b.data_ptr(), None, None, None, y.data_ptr(), y.stride(0),
+            y.stride(1), None, B, Tp, Cp, co, k, _hip.i32_array([j * dilation for j in range(k)]), 1, 0, 1.0, 0,
+            _hip.F32, _hip.stream_ptr(self.dev)), "itts_igemm_fwd")
+        return y
+
+    def relu_bn(self, x: torch.Tensor, name: str, out: Optional[torch.Tensor] = None, eps: float = 1e-5):
+        """BatchNorm1d(eval)(relu(x)) over the channels of x [B, T, C] (unit channel stride), as one
+        folded affine map; out may be x itself or a strided view."""
+        ent = self._packed.get(("bn", name))
+        if ent is None:
+            sc = self.sd[name + ".weight"].float() / torch.sqrt(self.sd[name + ".running_var"].float() + eps)
+            ent = self._packed[("bn", name)] = (sc.contiguous(),
+                                               (self.sd[name + ".bias"].float() -
+                                                self.sd[name + ".running_mean"].float() * sc).contiguous())
+        sc, sh = ent
+        B, T, C = x.shape
+        y = torch.empty(B, T, C, dtype=torch.float32, device=self.dev) if out is None else out
+        _hip.check(self.lib.itts_relu_affine_rows(x.data_ptr(), x.stride(0), x.stride(1), B, T, C, sc.data_ptr(),
+                                                  sh.data_ptr(), y.data_ptr(), y.stride(0), y.stride(1),
+                                                  _hip.stream_ptr(self.dev)), "itts_relu_affine_rows")
+        return y
+
+    def tdnn(self, x: torch.Tensor, name: str, dilation: int = 1, x2: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """TDNNBlock = BN(ReLU(conv(x (+ x2)))) with speechbrain's reflect "same" padding, channel-last."""
+        w = self.sd[name + ".conv.conv.weight"]
+        k = w.shape[-1]
+        T = x.shape[1]
+        if k == 1 and x2 is None:
+            y = self(x, name + ".conv.conv")
+        else:
+            y = self.conv_taps(self.pad_rows(x, dilation * (k - 1) // 2, True, x2), name + ".conv.conv", dilation)
+            y = y[:, :T]
+        return self.relu_bn(y, name + ".norm.norm", out=out)

@@ -431,3 +431,32 @@ def test_igemm_splitk_matches_linear(M, K, N):
     bound = 1e-4 * (xq.abs() @ wq.abs().t()) + 1e-5
     assert bool(((got - want).abs() <= bound).all()), float((got - want).abs().max())
     assert bool(((bank(x.cuda(), "l").cpu() - got).abs() <= bound).all())
+
+
+@pytest.mark.parametrize("B,T,H,lens", [(2, 255, 8, None), (3, 40, 2, [40, 17, 1]), (1, 70, 4, [0])])
+def test_cond_rel_attn_matches_torch(B, T, H, lens):
+    """itts_cond_rel_attn vs the f32 torch restatement of RelPositionMultiHeadedAttention
+    (conditioning._rel_pos_mha's math: masked_fill(-inf), softmax, masked_fill(0)): |err| <= 2e-5."""
+    import math
+    _hip, lib = _lib()
+    g = torch.Generator().manual_seed(B * T + H)
+    C = 64 * H
+    qkv = torch.randn(B, T, 3 * C, generator=g)
+    pos = torch.randn(T, C, generator=g)
+    u, v = torch.randn(H, 64, generator=g) * 0.3, torch.randn(H, 64, generator=g) * 0.3
+    L = torch.tensor(lens if lens is not None else [T] * B, dtype=torch.int32)
+    q, k, vv = qkv.split(C, -1)
+    q = q.view(B, T, H, 64)
+    k, vv = k.view(B, T, H, 64).transpose(1, 2), vv.view(B, T, H, 64).transpose(1, 2)
+    pp = pos.view(1, T, H, 64).transpose(1, 2)
+    sc = ((q + u).transpose(1, 2) @ k.transpose(-2, -1) + (q + v).transpose(1, 2) @ pp.transpose(-2, -1)) / math.sqrt(64)
+    masked = (torch.arange(T)[None, :] >= L[:, None].long())[:, None, None, :]
+    att = torch.softmax(sc.masked_fill(masked, float("-inf")), -1).masked_fill(masked, 0.0)
+    want = (att @ vv).transpose(1, 2).reshape(B, T, C)
+    out = torch.empty(B, T, C, device="cuda")
+    qg, pg, ug, vg, lg = qkv.cuda(), pos.cuda(), u.cuda(), v.cuda(), L.cuda()
+    _hip.check(lib.itts_cond_rel_attn(qg.data_ptr(), 3 * C, pg.data_ptr(), C, ug.data_ptr(), vg.data_ptr(),
+                                      None if lens is None else lg.data_ptr(), B, T, H, 0.125, out.data_ptr(), C,
+                                      _hip.F32, _hip.stream_ptr()), "rel_attn")
+    got = out.cpu()
+    assert float((got - want).abs().max()) <= 2e-5, float((got - want).abs().max())
