@@ -176,6 +176,12 @@ int itts_pad_rows_bf16(const float* x, int64_t x_sb, int64_t ldx, const float* x
                        int T, int C, int pad, int reflect, int Cp, void* y, void* stream);
 int itts_relu_affine_rows(const float* x, int64_t x_sb, int64_t ldx, int B, int T, int C, const float* scale,
                           const float* shift, float* y, int64_t y_sb, int64_t ldy, void* stream);
+/* itts_time_stats -- ECAPA pooling statistics (BigVGAN/ECAPA_TDNN.py AttentiveStatisticsPooling /
+ * SEBlock means): per (b, c), w[t] = softmax_t(logits[b][t][c]) or 1/T (logits null); mean[b][c] =
+ * sum_t w x[b][t][c], std[b][c] = sqrt(max(sum_t w (x - mean)^2, eps)) (std may be null).  t in order:
+ * an utterance's statistics do not depend on the batch. */
+int itts_time_stats(const float* x, int64_t x_sb, int64_t ldx, const float* logits, int64_t l_sb, int64_t ldl, int B,
+                    int T, int C, float eps, float* mean, float* stdv, void* stream);
 /* itts_cond_rel_attn -- RelPositionMultiHeadedAttention (gpt/conformer/attention.py:235-312, no rel_shift),
  * head dim 64, H heads (C = 64 H): qkv f32 [B][T][ld_qkv] = (q | k | v) linear outputs, pos f32 [T][ld_pos]
  * = linear_pos(pos_emb), bias_u / bias_v [H][64]; score = ((q+u).k + (q+v).p) * scale over keys t < lens[b]

@@ -346,7 +346,54 @@ __global__ __launch_bounds__(256) void relu_affine_kernel(const float* __restric
   y[(int64_t)b * y_sb + (int64_t)t * ldy + c] = fmaf(fmaxf(v, 0.f), scale[c], shift[c]);
 }
 
+// ECAPA pooling statistics over time, one thread per (utterance, channel), t in order (fixed
+// rounding, independent of the batch): weights w = softmax over t of logits[b][t][c]
+// (AttentiveStatisticsPooling's attention) or 1/T when logits is null (the global context / SE mean);
+// mean = sum w x, std = sqrt(max(sum w (x - mean)^2, eps)) (BigVGAN/ECAPA_TDNN.py _compute_statistics).
+__global__ __launch_bounds__(256) void time_stats_kernel(const float* __restrict__ x, int64_t x_sb, int64_t ldx,
+                                                         const float* __restrict__ lg, int64_t l_sb, int64_t ldl,
+                                                         int T, int C, float eps, float* __restrict__ mean,
+                                                         float* __restrict__ stdv) {
+  const int c = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (c >= C) return;
+  const float* xr = x + (int64_t)b * x_sb + c;
+  float mx = 0.f, den = (float)T;
+  const float* lr = lg ? lg + (int64_t)b * l_sb + c : nullptr;
+  if (lr) {
+    mx = -INFINITY;
+    for (int t = 0; t < T; ++t) mx = fmaxf(mx, lr[(int64_t)t * ldl]);
+    den = 0.f;
+    for (int t = 0; t < T; ++t) den += expf(lr[(int64_t)t * ldl] - mx);
+  }
+  const float inv = 1.f / den;
+  float m = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float w = lr ? expf(lr[(int64_t)t * ldl] - mx) * inv : inv;
+    m = fmaf(w, xr[(int64_t)t * ldx], m);
+  }
+  mean[(int64_t)b * C + c] = m;
+  if (!stdv) return;
+  float v = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float w = lr ? expf(lr[(int64_t)t * ldl] - mx) * inv : inv;
+    const float d = xr[(int64_t)t * ldx] - m;
+    v = fmaf(w, d * d, v);
+  }
+  stdv[(int64_t)b * C + c] = sqrtf(fmaxf(v, eps));
+}
+
 }  // namespace
+
+extern "C" int itts_time_stats(const float* x, int64_t x_sb, int64_t ldx, const float* logits, int64_t l_sb,
+                               int64_t ldl, int B, int T, int C, float eps, float* mean, float* stdv, void* stream) {
+  const char* fn = "itts_time_stats";
+  ITTS_REQUIRE(B >= 0 && T > 0 && C > 0, fn, "bad sizes (T > 0)");
+  if (B == 0) return 0;
+  ITTS_REQUIRE(x && mean, fn, "null pointer");
+  hipLaunchKernelGGL(time_stats_kernel, dim3((C + 255) / 256, B), dim3(256), 0, itts::as_stream(stream), x, x_sb, ldx,
+                     logits, l_sb, ldl, T, C, eps, mean, stdv);
+  return itts::check_launch(fn);
+}
 
 extern "C" int itts_pad_rows_bf16(const float* x, int64_t x_sb, int64_t ldx, const float* x2, int64_t x2_sb,
                                   int64_t ldx2, int B, int T, int C, int pad, int reflect, int Cp, void* y,

@@ -48,6 +48,7 @@ SIGNATURES = {
     "itts_pad_rows_bf16": (_c_i, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_i, _c_i, _c_i, _vp,
                                   _vp]),
     "itts_relu_affine_rows": (_c_i, [_vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _vp, _c_i64, _c_i64, _vp]),
+    "itts_time_stats": (_c_i, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_f, _vp, _vp, _vp]),
     "itts_cond_rel_attn": (_c_i, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_f, _vp, _c_i64, _c_i,
                                   _vp]),
     "itts_cond_subsample": (_c_i, [_vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _c_i, _vp, _vp]),

@@ -257,3 +257,17 @@ class HipLinearBank:
             y = self.conv_taps(self.pad_rows(x, dilation * (k - 1) // 2, True, x2), name + ".conv.conv", dilation)
             y = y[:, :T]
         return self.relu_bn(y, name + ".norm.norm", out=out)
+
+    def time_stats(self, x: torch.Tensor, logits: Optional[torch.Tensor] = None, want_std: bool = True,
+                   eps: float = 1e-12):
+        """(mean, std) over time of x [B, T, C] f32 with softmax_t(logits [B, T, C]) or uniform weights;
+        one thread per (utterance, channel), row-independent (itts_time_stats)."""
+        B, T, C = x.shape
+        assert x.stride(2) == 1 and (logits is None or (logits.shape == x.shape and logits.stride(2) == 1))
+        mean = torch.empty(B, C, dtype=torch.float32, device=self.dev)
+        std = torch.empty(B, C, dtype=torch.float32, device=self.dev) if want_std else None
+        _hip.check(self.lib.itts_time_stats(
+            x.data_ptr(), x.stride(0), x.stride(1), _hip.ptr(logits), 0 if logits is None else logits.stride(0),
+            0 if logits is None else logits.stride(1), B, T, C, eps, mean.data_ptr(), _hip.ptr(std),
+            _hip.stream_ptr(self.dev)), "itts_time_stats")
+        return mean, std

@@ -93,8 +93,8 @@ def speaker_embedding(sd, mel_ref, prefix="speaker_encoder", lin=None):
 # convolution on the MFMA igemm (k > 1 as taps over reflect-padded bf16 rows), ReLU + eval BatchNorm
 # as one affine kernel, the Res2Net branches written into their slices of one buffer (no cat), and the
 # attentive pooling's global-context concat folded into a per-row bias of its first 1x1 conv; the
-# small per-utterance linears (SE, context, fc) on the same row-independent GEMM, so an utterance's
-# embedding does not depend on its batch.  The reference's fp16 mode runs this module under autocast
+# small per-utterance linears (SE, context, fc) on the same row-independent GEMM and the statistics
+# over time in one kernel (itts_time_stats), so an utterance's embedding does not depend on its batch.  The reference's fp16 mode runs this module under autocast
 # (infer.py:613-623).
 
 def _se_res2net_cl(x, sd, p, dilation, ops, scale=8):
@@ -108,15 +108,9 @@ def _se_res2net_cl(x, sd, p, dilation, ops, scale=8):
         ops.tdnn(h[..., i * w:(i + 1) * w], f"{p}.res2net_block.blocks.{i - 1}", dilation, x2=prev,
                  out=cat[..., i * w:(i + 1) * w])
     h = ops.tdnn(cat, p + ".tdnn2")
-    s = F.relu(ops(h.mean(dim=1), p + ".se_block.conv1.conv"))
+    s = F.relu(ops(ops.time_stats(h, want_std=False)[0], p + ".se_block.conv1.conv"))
     s = torch.sigmoid(ops(s, p + ".se_block.conv2.conv"))
     return torch.addcmul(x, h, s[:, None, :])
-
-
-def _stats_cl(x, w, eps=1e-12):
-    mean = (w * x).sum(1)
-    std = torch.sqrt((w * (x - mean.unsqueeze(1)).pow(2)).sum(1).clamp(eps))
-    return mean, std
 
 
 def speaker_embedding_cl(sd, mel_ref, ops, prefix="speaker_encoder"):
@@ -129,7 +123,7 @@ def speaker_embedding_cl(sd, mel_ref, ops, prefix="speaker_encoder"):
         feats.append(x)
     x = ops.tdnn(torch.cat(feats, dim=-1), prefix + ".mfa")
     B, L, C = x.shape
-    mean, std = _stats_cl(x, torch.full((1, L, 1), 1.0 / L, dtype=x.dtype, device=x.device))
+    mean, std = ops.time_stats(x)
     # tdnn(cat([x, mean, std])) = W_x x + (W_m mean + W_s std + b): the context as a per-row bias
     q = prefix + ".asp.tdnn"
     key = q + ".conv.conv"
@@ -140,8 +134,7 @@ def speaker_embedding_cl(sd, mel_ref, ops, prefix="speaker_encoder"):
     pb = ops(torch.cat([mean, std], -1), key + ".ctx")
     a = ops(x, key + ".x", bias=False) + pb[:, None, :]
     a = torch.tanh(ops.relu_bn(a, q + ".norm.norm"))
-    # softmax over time: on the [B, C, T] transpose (a last-dim softmax), read back as a strided view
-    a = torch.softmax(ops(a, prefix + ".asp.conv.conv").transpose(1, 2).contiguous(), dim=-1).transpose(1, 2)
-    mean, std = _stats_cl(x, a)
+    # softmax over time and the weighted statistics in one row-independent kernel
+    mean, std = ops.time_stats(x, ops(a, prefix + ".asp.conv.conv"))
     pooled = _bn(torch.cat([mean, std], dim=1).unsqueeze(2), sd, prefix + ".asp_bn.norm")[:, :, 0]
     return ops(pooled, prefix + ".fc.conv")
