@@ -346,40 +346,60 @@ __global__ __launch_bounds__(256) void relu_affine_kernel(const float* __restric
   y[(int64_t)b * y_sb + (int64_t)t * ldy + c] = fmaf(fmaxf(v, 0.f), scale[c], shift[c]);
 }
 
-// ECAPA pooling statistics over time, one thread per (utterance, channel), t in order (fixed
-// rounding, independent of the batch): weights w = softmax over t of logits[b][t][c]
-// (AttentiveStatisticsPooling's attention) or 1/T when logits is null (the global context / SE mean);
-// mean = sum w x, std = sqrt(max(sum w (x - mean)^2, eps)) (BigVGAN/ECAPA_TDNN.py _compute_statistics).
-__global__ __launch_bounds__(256) void time_stats_kernel(const float* __restrict__ x, int64_t x_sb, int64_t ldx,
-                                                         const float* __restrict__ lg, int64_t l_sb, int64_t ldl,
-                                                         int T, int C, float eps, float* __restrict__ mean,
-                                                         float* __restrict__ stdv) {
-  const int c = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
-  if (c >= C) return;
-  const float* xr = x + (int64_t)b * x_sb + c;
-  float mx = 0.f, den = (float)T;
-  const float* lr = lg ? lg + (int64_t)b * l_sb + c : nullptr;
+// ECAPA pooling statistics over time (BigVGAN/ECAPA_TDNN.py _compute_statistics): weights w =
+// softmax over t of logits[b][t][c] (AttentiveStatisticsPooling's attention) or 1/T when logits is
+// null (the global context / SE mean); mean = sum w x, std = sqrt(max(sum w (x - mean)^2, eps)).
+// A workgroup = 64 channels x 16 time slices of one utterance; each pass combines the 16 slice
+// partials in slice order through LDS (fixed rounding, independent of the batch).
+__device__ __forceinline__ float slice_combine(float v, float* red, bool is_max) {
+  const int ci = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  __syncthreads();  // previous readers of red are done
+  red[sl * 64 + ci] = v;
+  __syncthreads();
+  float acc = red[ci];
+  for (int k = 1; k < 16; ++k) acc = is_max ? fmaxf(acc, red[k * 64 + ci]) : acc + red[k * 64 + ci];
+  return acc;
+}
+
+__global__ __launch_bounds__(1024) void time_stats_kernel(const float* __restrict__ x, int64_t x_sb, int64_t ldx,
+                                                          const float* __restrict__ lg, int64_t l_sb, int64_t ldl,
+                                                          int T, int C, float eps, float* __restrict__ mean,
+                                                          float* __restrict__ stdv) {
+  __shared__ float red[16 * 64];
+  const int ci = threadIdx.x & 63, sl = threadIdx.x >> 6, c = blockIdx.x * 64 + ci, b = blockIdx.y;
+  const bool on = c < C;
+  const int per = (T + 15) / 16, t0 = sl * per, t1 = min(T, t0 + per);
+  const float* xr = x + (int64_t)b * x_sb + (on ? c : 0);
+  const float* lr = lg ? lg + (int64_t)b * l_sb + (on ? c : 0) : nullptr;
+  float mx = 0.f, inv = 1.f / (float)T;
   if (lr) {
-    mx = -INFINITY;
-    for (int t = 0; t < T; ++t) mx = fmaxf(mx, lr[(int64_t)t * ldl]);
-    den = 0.f;
-    for (int t = 0; t < T; ++t) den += expf(lr[(int64_t)t * ldl] - mx);
+    float m = -INFINITY;
+    if (on)
+      for (int t = t0; t < t1; ++t) m = fmaxf(m, lr[(int64_t)t * ldl]);
+    mx = slice_combine(m, red, true);
+    float d = 0.f;
+    if (on)
+      for (int t = t0; t < t1; ++t) d += expf(lr[(int64_t)t * ldl] - mx);
+    inv = 1.f / slice_combine(d, red, false);
   }
-  const float inv = 1.f / den;
   float m = 0.f;
-  for (int t = 0; t < T; ++t) {
-    const float w = lr ? expf(lr[(int64_t)t * ldl] - mx) * inv : inv;
-    m = fmaf(w, xr[(int64_t)t * ldx], m);
-  }
-  mean[(int64_t)b * C + c] = m;
-  if (!stdv) return;
+  if (on)
+    for (int t = t0; t < t1; ++t) {
+      const float w = lr ? expf(lr[(int64_t)t * ldl] - mx) * inv : inv;
+      m = fmaf(w, xr[(int64_t)t * ldx], m);
+    }
+  m = slice_combine(m, red, false);
+  if (on && sl == 0) mean[(int64_t)b * C + c] = m;
+  if (!stdv) return;  // uniform per launch
   float v = 0.f;
-  for (int t = 0; t < T; ++t) {
-    const float w = lr ? expf(lr[(int64_t)t * ldl] - mx) * inv : inv;
-    const float d = xr[(int64_t)t * ldx] - m;
-    v = fmaf(w, d * d, v);
-  }
-  stdv[(int64_t)b * C + c] = sqrtf(fmaxf(v, eps));
+  if (on)
+    for (int t = t0; t < t1; ++t) {
+      const float w = lr ? expf(lr[(int64_t)t * ldl] - mx) * inv : inv;
+      const float dd = xr[(int64_t)t * ldx] - m;
+      v = fmaf(w, dd * dd, v);
+    }
+  v = slice_combine(v, red, false);
+  if (on && sl == 0) stdv[(int64_t)b * C + c] = sqrtf(fmaxf(v, eps));
 }
 
 }  // namespace
@@ -390,7 +410,7 @@ extern "C" int itts_time_stats(const float* x, int64_t x_sb, int64_t ldx, const 
   ITTS_REQUIRE(B >= 0 && T > 0 && C > 0, fn, "bad sizes (T > 0)");
   if (B == 0) return 0;
   ITTS_REQUIRE(x && mean, fn, "null pointer");
-  hipLaunchKernelGGL(time_stats_kernel, dim3((C + 255) / 256, B), dim3(256), 0, itts::as_stream(stream), x, x_sb, ldx,
+  hipLaunchKernelGGL(time_stats_kernel, dim3((C + 63) / 64, B), dim3(1024), 0, itts::as_stream(stream), x, x_sb, ldx,
                      logits, l_sb, ldl, T, C, eps, mean, stdv);
   return itts::check_launch(fn);
 }

@@ -40,7 +40,8 @@ def load(d, counter):
 
 
 def short(name):
-    for k in sorted(DECODE_KERNELS, key=len, reverse=True) + ["igemm_kernel", "amp_conv_kernel", "aa_snakebeta_kernel",
+    for k in sorted(DECODE_KERNELS, key=len, reverse=True) + ["igemm256_kernel", "igemm_kernel", "amp_conv_kernel",
+                                                              "aa_snakebeta_kernel",
                                                               "aa_snake_mfma_kernel"]:
         if k in name:
             return k
@@ -49,7 +50,7 @@ def short(name):
 
 def vocoder(fetch, write):
     out = {"kernel": "igemm_kernel (BigVGAN convs, second of two C3 vocoder forwards)"}
-    groups = {"igemm_kernel": lambda n: "igemm_kernel" in n,
+    groups = {"igemm_kernel": lambda n: "igemm_kernel" in n or "igemm256_kernel" in n,  # both tile families
               "amp_conv_kernel": lambda n: "amp_conv_kernel" in n,  # conv-only and act-fused forms
               # the activation: MFMA kernel on the vocoder's bf16 channel-last layout (VALU kernel otherwise)
               "aa_snakebeta_kernel": lambda n: "aa_snakebeta_kernel" in n or "aa_snake_mfma_kernel" in n}

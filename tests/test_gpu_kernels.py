@@ -460,3 +460,22 @@ def test_cond_rel_attn_matches_torch(B, T, H, lens):
                                       _hip.F32, _hip.stream_ptr()), "rel_attn")
     got = out.cpu()
     assert float((got - want).abs().max()) <= 2e-5, float((got - want).abs().max())
+
+
+@pytest.mark.parametrize("B,T,C,att", [(2, 511, 1536, True), (3, 37, 100, False), (1, 5, 64, True)])
+def test_time_stats_matches_torch(B, T, C, att):
+    """itts_time_stats vs the f32 torch restatement of ECAPA's _compute_statistics (softmax weights or
+    uniform 1/T): |err| <= 1e-5 relative; row-independent (a batch's rows equal the rows alone)."""
+    from indextts.utils.hiplinear import HipLinearBank
+    g = torch.Generator().manual_seed(B * T + C)
+    x = torch.randn(B, T, C, generator=g) * 2 + 0.5
+    lg = torch.randn(B, T, C, generator=g) * 3 if att else None
+    w = torch.softmax(lg, dim=1) if att else torch.full((1, T, 1), 1.0 / T)
+    mean = (w * x).sum(1)
+    std = torch.sqrt((w * (x - mean[:, None]) ** 2).sum(1).clamp(1e-12))
+    bank = HipLinearBank({}, "cuda")
+    gm, gs = bank.time_stats(x.cuda(), None if lg is None else lg.cuda())
+    assert float(((gm.cpu() - mean).abs() / (mean.abs() + 1)).max()) <= 1e-5
+    assert float(((gs.cpu() - std).abs() / (std.abs() + 1)).max()) <= 1e-5
+    m1, s1 = bank.time_stats(x[-1:].cuda(), None if lg is None else lg[-1:].cuda())
+    assert torch.equal(m1[0], gm[-1]) and torch.equal(s1[0], gs[-1])
