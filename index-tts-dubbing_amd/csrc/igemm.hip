@@ -571,6 +571,12 @@ int ig256_variant() {
   return v;
 }
 
+// Cout = 192 on whole-width 256 x 192 tiles (read per launch: A/B in one process)
+bool ig192_enabled() {
+  const char* e = getenv("ITTS_IG192");
+  return e ? atoi(e) != 0 : true;
+}
+
 // ITTS_IGEMM_WIN=0 keeps the per-tap A tiles (A/B measurements)
 bool igemm_win_enabled() {
   static const bool on = [] {
@@ -631,8 +637,10 @@ void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
   if (g256) {
     const int v = ig256_variant();
     const bool k64 = a.ci_pad % 64 == 0;
-    if (a.Cout % 128 != 0) {  // Cout = 192 (generator stage 2): 256 x 64 tiles, 4 x 2 waves of 64 x 32
-      if (k64) launch256<64, 4, 2, 64, 2, OutT>(a, s);
+    if (a.Cout % 128 != 0) {  // Cout = 192 (generator stage 2)
+      // 256 x 192 tiles, 4 x 2 waves of 64 x 96 (ITTS_IG192=1) or 256 x 64 tiles of 64 x 32
+      if (k64 && a.Cout == 192 && ig192_enabled()) launch256<192, 4, 2, 64, 2, OutT>(a, s);
+      else if (k64) launch256<64, 4, 2, 64, 2, OutT>(a, s);
       else dispatch_old<OutT>(a, vec, s);
       return;
     }

@@ -324,3 +324,30 @@ def test_amp_conv_matches_torch(C, k, d, use_act, nres, alpha):
         scale = alpha * F.conv1d(xb.abs(), wq.abs(), dilation=d, padding=d * (k - 1) // 2)[0].t()
         err = (y[b, :L].float().cpu() - ref).abs()
         assert bool((err <= 2e-2 * scale + 1e-2 * ref.abs() + 1e-3).all()), (b, float(err.max()))
+
+
+@pytest.mark.parametrize("cin,k,d", [(192, 11, 5), (192, 3, 1), (384, 1, 1)])
+def test_igemm_cout192_whole_width_tile_equals_64_column_tiles(monkeypatch, cin, k, d):
+    """Cout = 192 (generator stage 2) on 256 x 192 tiles (default) is bit-identical to the 256 x 64
+    tiles (ITTS_IG192=0): the same K-step order (channel chunk, tap) and MFMA blocks per output.
+    bf16 output with both residuals and alpha, as the AMP layers call it; ragged lengths."""
+    from indextts.vocoder.bigvgan import _Conv, conv1d_taps
+    _hip, lib = _lib()
+    torch.manual_seed(cin + k)
+    B, T, cout = 3, 3000, 192
+    lens = torch.tensor([3000, 1, 1234], dtype=torch.int32).cuda()
+    x = torch.randn(B, T, cin).to(torch.bfloat16).cuda()
+    r1, r2 = (torch.randn(B, T, cout).to(torch.bfloat16).cuda() for _ in range(2))
+    conv = _Conv(*conv1d_taps(torch.randn(cout, cin, k) / (cin * k) ** 0.5, d), torch.randn(cout) * 0.1,
+                 cin, cout, "cuda")
+    outs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("ITTS_IG192", v)
+        y = torch.full((B, T, cout), 3.0, dtype=torch.bfloat16, device="cuda")
+        _hip.check(lib.itts_igemm_fwd(x.data_ptr(), T * cin, cin, conv.w.data_ptr(), conv.bias.data_ptr(), None,
+                                      r1.data_ptr(), r2.data_ptr(), y.data_ptr(), T * cout, cout, lens.data_ptr(), B,
+                                      T, cin, cout, conv.ntaps, conv.offs, 1, 0, 0.5, 0, _hip.BF16,
+                                      _hip.stream_ptr()), "igemm")
+        torch.cuda.synchronize()
+        outs.append(y)
+    assert torch.equal(outs[0], outs[1])
