@@ -114,10 +114,13 @@ typedef struct ItTsAmpLayer {  /* one AMPBlock1 dilation: x' = c2(a2(c1(a1(x))))
   ItTsConv c2;
 } ItTsAmpLayer;
 typedef struct ItTsBigvganStage {
-  int up_rate;                 /* ConvTranspose1d stride u: u polyphase convs */
-  const ItTsConv* phases;      /* [up_rate] */
-  const float* cond_w;         /* conds[i] (1x1 on the speaker embedding): [cout][spk_dim] f32 */
-  const float* cond_b;         /* [cout] */
+  int up_rate;                 /* ConvTranspose1d stride u */
+  const ItTsConv* phases;      /* [up_rate] polyphase convs (phase rho writes rows q*u + rho), OR [1]: one
+                                  conv with cout = u * C (C = layers' channels) whose output column block
+                                  rho is phase rho -- row q of its [T][u*C] output = rows q*u .. q*u+u-1 */
+  const float* cond_w;         /* conds[i] (1x1 on the speaker embedding): [phases[0].cout][spk_dim] f32
+                                  (the fused form repeats the C rows u times) */
+  const float* cond_b;         /* [phases[0].cout] */
   int n_blocks, n_layers;      /* resblocks (kernel sizes) x dilations */
   const ItTsAmpLayer* layers;  /* [n_blocks][n_layers] */
   int amp_mode;                /* 0: act kernel + implicit-GEMM conv; 1: act fused into itts_amp_conv_fwd;

@@ -33,6 +33,18 @@ __global__ void scale_lengths_kernel(const int32_t* __restrict__ lens, int32_t* 
 
 int64_t align256(int64_t v) { return (v + 255) / 256 * 256; }
 
+// A stage's up-sampler is either up_rate phase convs (phase rho writes rows q*u + rho) or ONE conv
+// whose cout = up_rate * C holds the phases as output column blocks (row q of the [T][u*C] output is
+// rows q*u .. q*u+u-1 of the [T*u][C] stage input): fused when phases[0].cout == u * C, C the AMP
+// layers' channel count.
+bool fused_up(const ItTsBigvganStage& st) {
+  return st.up_rate > 1 && st.n_blocks > 0 && st.n_layers > 0 && st.layers &&
+         st.phases[0].cout == st.up_rate * st.layers[0].c1.cout;
+}
+int stage_channels(const ItTsBigvganStage& st) {
+  return fused_up(st) ? st.phases[0].cout / st.up_rate : st.phases[0].cout;
+}
+
 struct Layout {
   int64_t lens, pre_b, stage_b[kMaxStages], bufs[6], total, buf_elems;
 };
@@ -51,7 +63,7 @@ bool layout(const ItTsBigvganWeights* w, int B, int T, Layout& L) {
     L.stage_b[i] = off;
     off = align256(off + (int64_t)B * st.phases[0].cout * 4);
     t *= st.up_rate;
-    const int64_t e = (int64_t)B * t * st.phases[0].cout;
+    const int64_t e = (int64_t)B * t * stage_channels(st);
     maxe = e > maxe ? e : maxe;
   }
   L.buf_elems = maxe;
@@ -125,12 +137,15 @@ extern "C" int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* lat
   int Tcur = T;
   for (int i = 0; i < ns && rc == 0; ++i) {
     const ItTsBigvganStage& st = w->stages[i];
-    const int u = st.up_rate, C = st.phases[0].cout, Tn = Tcur * u;
+    const int u = st.up_rate, C = stage_channels(st), Tn = Tcur * u;
     const int32_t* ln_in = lens + (int64_t)i * B;
     const int32_t* ln = lens + (int64_t)(i + 1) * B;
     const float* sb = reinterpret_cast<const float*>(ws + L.stage_b[i]);
-    for (int rho = 0; rho < u && rc == 0; ++rho)
-      rc = conv(st.phases[rho], cur_in, Tcur, xst, Tn, ln_in, nullptr, nullptr, 1.0f, sb, u, rho);
+    if (fused_up(st))  // [B][Tcur][u*C] output rows are the [B][Tn][C] rows, speaker bias per phase block
+      rc = conv(st.phases[0], cur_in, Tcur, xst, Tcur, ln_in, nullptr, nullptr, 1.0f, sb, 1, 0);
+    else
+      for (int rho = 0; rho < u && rc == 0; ++rho)
+        rc = conv(st.phases[rho], cur_in, Tcur, xst, Tn, ln_in, nullptr, nullptr, 1.0f, sb, u, rho);
     uint16_t* xs = (i % 2 == 0) ? xs_b : xs_a;
     for (int j = 0; j < st.n_blocks && rc == 0; ++j) {
       const uint16_t* src = xst;
@@ -161,7 +176,7 @@ extern "C" int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* lat
     Tcur = Tn;
   }
   if (rc) return rc;
-  const int Cl = w->stages[ns - 1].phases[0].cout;
+  const int Cl = stage_channels(w->stages[ns - 1]);
   const int32_t* ln = lens + (int64_t)ns * B;
   rc = act(w->act_post, cur_in, t1, Cl, Tcur, ln);
   if (rc) return rc;

@@ -7,7 +7,8 @@ reference's ``infer()``).
 
 HBM layout: channel-last ``[B, T_stage, C]`` bf16 activations (T_stage = T * prod(upsample rates so
 far)); weights prepacked once as bf16 ``[taps][co_pad][ci_pad]`` for the MFMA implicit-GEMM kernel.
-Per stage:  ConvTranspose1d (u polyphase launches; + conds[i](spk) as a per-utterance bias)
+Per stage:  ConvTranspose1d (u polyphase convs, or ONE implicit GEMM with the phases as output
+            columns; + conds[i](spk) as a per-utterance bias)
             -> 3 AMPBlock1, each 3 x [act -> conv(dil) -> act -> conv + residual]; the third conv of
                each block also accumulates the block sum and applies the 1/3 mean in its epilogue.
 Tail: activation_post -> conv_post + tanh (+ int16 conversion of ``infer()``) in one kernel.
@@ -97,6 +98,24 @@ def convtr_phases(w: torch.Tensor, u: int, padding: int):
     return phases
 
 
+def convtr_fused(w: torch.Tensor, u: int, padding: int):
+    """ConvTranspose1d as ONE implicit GEMM whose output columns are the u phases: the [T*u][co]
+    output viewed as [T][u*co] (row q = output samples u*q .. u*q+u-1, column block rho = phase rho).
+    Taps: the union of the phases' input offsets; a phase's block of a tap matrix [u*co, ci] is zero at
+    offsets the phase does not use.  The input is read once instead of once per phase."""
+    ph = convtr_phases(w, u, padding)
+    co, ci = ph[0][0][0].shape
+    offs = sorted({o for _, oo in ph for o in oo})
+    taps = []
+    for o in offs:
+        m = torch.zeros(u * co, ci, dtype=torch.float32)
+        for rho, (tt, oo) in enumerate(ph):
+            if o in oo:
+                m[rho * co:(rho + 1) * co] = tt[oo.index(o)]
+        taps.append(m)
+    return taps, offs
+
+
 class _Conv:
     def __init__(self, taps, offs, bias, cin, cout, device):
         self.w = pack_taps(taps, cin, cout).to(device)
@@ -137,13 +156,18 @@ class HipBigVGAN:
         w = sd["conv_pre.weight"]
         taps, offs = conv1d_taps(w)
         self.conv_pre = _Conv(taps, offs, sd["conv_pre.bias"], w.shape[1], w.shape[0], dev)
-        self.ups = []
+        self.ups = []  # (u, convs, C): u phase convs, or ONE conv with the phases as output columns
         for i, (u, k) in enumerate(zip(h.upsample_rates, h.upsample_kernel_sizes)):
             wt = sd[f"ups.{i}.0.weight"]
             u, k = int(u), int(k)
-            phases = [(_Conv(t, o, sd[f"ups.{i}.0.bias"], wt.shape[0], wt.shape[1], dev)) for t, o in
-                      convtr_phases(wt, u, (k - u) // 2)]
-            self.ups.append((u, phases))
+            ci, co = wt.shape[0], wt.shape[1]
+            bias = sd[f"ups.{i}.0.bias"]
+            if self._fuse_convtr(u, k, co):
+                taps, offs = convtr_fused(wt, u, (k - u) // 2)
+                convs = [_Conv(taps, offs, bias.reshape(-1).repeat(u), ci, u * co, dev)]
+            else:
+                convs = [_Conv(t, o, bias, ci, co, dev) for t, o in convtr_phases(wt, u, (k - u) // 2)]
+            self.ups.append((u, convs, co))
         self.nk = len(h.resblock_kernel_sizes)
         self.blocks = []
         for i in range(len(h.upsample_rates)):
@@ -175,6 +199,18 @@ class HipBigVGAN:
         self._cw = self._c_weights()
         self._ws = None
 
+    @staticmethod
+    def _fuse_convtr(u: int, k: int, co: int) -> bool:
+        """All phases in one launch where every phase uses the same input offsets (kernel == stride:
+        no extra MFMA work; stages 2 and 3: 4 x 252 -> 451 us and 4 x 85 -> 275 us).  The k = 2u stages
+        stay per phase: their offset union has 3 taps instead of 2 per phase (+50 % MFMA); measured at
+        C <= 96 too (96: 2 x 470 -> 830 us, 48: 2 x 380 -> 882 us, profiles/convt_ab_r03.txt).
+        ITTS_VOC_CONVT_FUSED=0: never; =2: also the narrow k = 2u stages (A/B)."""
+        mode = os.environ.get("ITTS_VOC_CONVT_FUSED", "1")
+        if u <= 1 or mode == "0":
+            return False
+        return k == u or (mode == "2" and co <= 96)
+
     # ---------------- the C-ABI description of this generator ----------------
     @staticmethod
     def _c_conv(c: "_Conv") -> "_hip.Conv":
@@ -199,18 +235,19 @@ class HipBigVGAN:
                 self._cond_w[name] = self.sd_torch[name + ".weight"][:, :, 0].float().contiguous()
         keep = []
         stages = (_hip.BigvganStage * len(self.ups))()
-        for i, (u, phases) in enumerate(self.ups):
-            ph = (_hip.Conv * u)(*[self._c_conv(c) for c in phases])
+        for i, (u, convs, C) in enumerate(self.ups):
+            ph = (_hip.Conv * len(convs))(*[self._c_conv(c) for c in convs])
+            rep = convs[0].cout // C  # fused phases: the speaker bias repeated per phase column block
             blocks = self.blocks[i]
             nl = len(blocks[0])
             lay = (_hip.AmpLayer * (len(blocks) * nl))()
             for j, layers in enumerate(blocks):
                 for n, (a1, c1, a2, c2) in enumerate(layers):
                     lay[j * nl + n] = _hip.AmpLayer(self._c_act(a1), self._c_conv(c1), self._c_act(a2), self._c_conv(c2))
-            cb = self.sd_torch[f"conds.{i}.bias"].float()
-            keep += [ph, lay, cb]
-            stages[i] = _hip.BigvganStage(u, ph, self._cond_w[f"conds.{i}"].data_ptr(), cb.data_ptr(), len(blocks), nl,
-                                          lay, self._amp_mode(phases[0].cout))
+            cb = self.sd_torch[f"conds.{i}.bias"].float().repeat(rep).contiguous()
+            cw = self._cond_w[f"conds.{i}"].repeat(rep, 1).contiguous()
+            keep += [ph, lay, cb, cw]
+            stages[i] = _hip.BigvganStage(u, ph, cw.data_ptr(), cb.data_ptr(), len(blocks), nl, lay, self._amp_mode(C))
         pb = self.sd_torch["cond_layer.bias"].float()
         keep += [stages, pb]
         w = _hip.BigvganWeights(len(self.ups), self.conv_pre.cin, self._cond_w["cond_layer"].shape[1],
@@ -334,13 +371,16 @@ class HipBigVGAN:
         cur_in = self._buf("xs_a", (B, T, C0))
         self._conv(self.conv_pre, x, cur_in, lens, bias_b=pre_b)
         Tcur = T
-        for i, (u, phases) in enumerate(self.ups):
-            C = phases[0].cout
+        for i, (u, convs, C) in enumerate(self.ups):
             Tn = Tcur * u
             lens_n = (lens * u).contiguous()
             x_st = self._buf("x", (B, Tn, C))
-            for rho, ph in enumerate(phases):
-                self._conv(ph, cur_in, x_st, lens, bias_b=stage_b[i], ymul=u, yoff=rho)
+            if len(convs) == 1 and u > 1:  # phases as output columns: [B][Tcur][u*C] is [B][Tn][C]
+                self._conv(convs[0], cur_in, x_st.view(B, Tcur, u * C), lens,
+                           bias_b=stage_b[i].repeat(1, u).contiguous())
+            else:
+                for rho, ph in enumerate(convs):
+                    self._conv(ph, cur_in, x_st, lens, bias_b=stage_b[i], ymul=u, yoff=rho)
             self.rows *= u
             t1 = self._buf("t1", (B, Tn, C))
             t2 = self._buf("t2", (B, Tn, C))

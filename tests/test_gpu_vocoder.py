@@ -351,3 +351,38 @@ def test_igemm_cout192_whole_width_tile_equals_64_column_tiles(monkeypatch, cin,
         torch.cuda.synchronize()
         outs.append(y)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("ci,co,k,u", [(192, 96, 4, 4), (96, 48, 4, 2), (48, 24, 4, 2), (384, 192, 4, 4),
+                                       (768, 384, 8, 4)])
+def test_convtranspose_phases_as_output_columns_matches_torch(ci, co, k, u):
+    """ConvTranspose1d(k, stride u, padding (k-u)/2) as ONE implicit GEMM with the u phases as output
+    column blocks (convtr_fused): the [T][u*co] output read as [T*u][co] equals torch's
+    conv_transpose1d on the bf16-rounded operands (f32 accumulation), per utterance of a ragged
+    batch; output rows past len*u are not written.  Tolerance as test_igemm_conv_matches_torch."""
+    from indextts.vocoder.bigvgan import _Conv, convtr_fused
+    _hip, lib = _lib()
+    torch.manual_seed(ci + k)
+    B, T = 2, 300
+    lens = torch.tensor([T, 77], dtype=torch.int32)
+    x = torch.randn(B, T, ci).to(torch.bfloat16)
+    w = torch.randn(ci, co, k) / (ci * k / u) ** 0.5
+    bias = torch.randn(co) * 0.1
+    taps, offs = convtr_fused(w, u, (k - u) // 2)
+    conv = _Conv(taps, offs, bias.repeat(u), ci, u * co, "cuda")
+    y = torch.full((B, T * u, co), 9.0, device="cuda")
+    xd, lensd = x.cuda(), lens.cuda()
+    _hip.check(lib.itts_igemm_fwd(xd.data_ptr(), T * ci, ci, conv.w.data_ptr(), conv.bias.data_ptr(), None, None,
+                                  None, y.data_ptr(), T * u * co, u * co, lensd.data_ptr(), B, T, ci, u * co,
+                                  conv.ntaps, conv.offs, 1, 0, 1.0, 0, _hip.F32, _hip.stream_ptr()), "igemm")
+    torch.cuda.synchronize()
+    wq = w.to(torch.bfloat16).float()
+    for b in range(B):
+        L = int(lens[b])
+        xb = x[b:b + 1, :L].float().transpose(1, 2)
+        ref = F.conv_transpose1d(xb, wq, bias, stride=u, padding=(k - u) // 2)[0].t()
+        scale = F.conv_transpose1d(xb.abs(), wq.abs(), stride=u, padding=(k - u) // 2)[0].t()
+        assert ref.shape[0] == L * u
+        err = (y[b, :L * u].cpu() - ref).abs()
+        assert bool((err <= 1e-4 * scale + 1e-5).all()), float(err.max())
+        assert bool((y[b, L * u:] == 9.0).all())
