@@ -583,12 +583,16 @@ int attn_decode_launch(const char* fn, const float* qkv, int64_t ldqkv, int nspl
   const uint16_t* wp = static_cast<const uint16_t*>(wproj);
   // keys per group per round: 10 (320 keys per workgroup round) for the 32-row steps, 4 for steps of
   // >= 128 rows (long-form chunks), whose 2048+ workgroups are occupancy-bound at 10 -- B = 128: S = 71
-  // 23.8 -> 15.5 us, S = 300 31.1 vs 31.7 (profiles/ubench_attn_kb_r03.txt)
+  // 23.8 -> 15.5 us, S = 300 31.1 vs 31.7 (profiles/ubench_attn_kb_r03.txt) -- and for the beam
+  // lineage form at any row count: its beams re-read a shared prefix out of L2, so 4 workgroups per CU
+  // (120 VGPRs) beat 2 (224): beam3 C3 757 -> 787 audio-s/s.  A per-utterance form (the beams of one
+  // utterance in one workgroup, each shared row loaded once) was slower still: 744
+  // (profiles/beam_attn_ab_r03.txt).
   static const bool small_ok = [] {  // ITTS_ATTN_SMALLKB=0: always 10 (A/B)
     const char* e = getenv("ITTS_ATTN_SMALLKB");
     return !(e && e[0] == '0');
   }();
-  const bool small_kb = small_ok && B >= 128 && !wproj;
+  const bool small_kb = small_ok && (B >= 128 || kv_rows) && !wproj;
 #define ITTS_AD1(TC, TO, PR, KBV)                                                                                     \
   do {                                                                                                            \
     if (kv_rows)                                                                                                  \
