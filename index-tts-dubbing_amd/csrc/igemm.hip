@@ -1,4 +1,4 @@
-// Implicit-GEMM on MFMA (v_mfma_f32_32x32x16_bf16) for gfx950: one kernel serves
+// Implicit-GEMM on MFMA for gfx950 (igemm256: v_mfma_f32_16x16x32_bf16; the register-staged igemm_kernel: 32x32x16): one kernel serves
 //   * BigVGAN Conv1d (dilated, zero "same" padding)      BigVGAN/models.py:24-42, utils.py:59-60
 //   * BigVGAN ConvTranspose1d as u polyphase convs        BigVGAN/models.py:155-161 (torch ConvTranspose1d)
 //   * conv_pre                                             BigVGAN/models.py:149,224
@@ -21,12 +21,16 @@
 // it at row offset off_j - min_off), instead of TM rows per tap: an 11-tap conv moves 178 input rows
 // per chunk through L2 -> LDS instead of 1408.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
 namespace {
 
 constexpr int kMaxTaps = 16;
+#ifndef ITTS_IG_MFMA16  // igemm256: 16x16x32 MFMA blocks (-DITTS_IG_MFMA16=0: 32x32x16, A/B build)
+#define ITTS_IG_MFMA16 1  // latent GEMMs +3-8 %, vocoder convs within noise (profiles/mfma16_ab_r03.txt)
+#endif
 constexpr int kWinSpan = 64;  // WIN: max tap span (rows)
 #ifndef ITTS_IG_WIN_MINTAPS  // fewest taps that take the window form
 #define ITTS_IG_WIN_MINTAPS 3
@@ -382,14 +386,22 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
     else wait_vm<0>();
   };
 
-  f32x16_t acc[FM][FN];
+  // MFMA16 (ITTS_IG_MFMA16, BK = 64): v_mfma_f32_16x16x32_bf16 on 16 x 16 blocks instead of 32 x 32 x 16
+  // (the same LDS fragment bytes per K step; MI355X_MICROARCH.md measures the 16x16x32 form at
+  // 1.12-1.15x the 32x32x16 FLOP rate with LDS operands)
+  constexpr bool M16 = ITTS_IG_MFMA16 && BK == 64;
+  constexpr int AM = M16 ? 2 * FM : FM, AN = M16 ? 2 * FN : FN;
+  typedef typename std::conditional<M16, f32x4_t, f32x16_t>::type acc_t;
+  constexpr int AR = M16 ? 4 : 16;
+  acc_t acc[AM][AN];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int i = 0; i < AM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < AN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < AR; ++r) acc[i][j][r] = 0.f;
   const int r32 = lane & 31, h = lane >> 5;
+  const int r16 = lane & 15, qg = lane >> 4;
   auto compute = [&](int it) {
     const unsigned char* As = smem + (it % NSLOT) * STAGE;
     const unsigned char* Bs = As + A_BYTES;
@@ -400,23 +412,46 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
       Bs = smem + 2 * W_BYTES + (it & 1) * B_BYTES;
       arow = p.tap_off[j] - p.min_off;
     }
+    if constexpr (M16) {
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      bf16x8_t af[FM], bfr[FN];
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8_t af[AM], bfr[AN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int row = arow + wm + 32 * i + r32;
-        af[i] = *reinterpret_cast<const bf16x8_t*>(As + row * ROWB + (((2 * ks + h) ^ swz(row)) << 4));
+        for (int i = 0; i < AM; ++i) {
+          const int row = arow + wm + 16 * i + r16;
+          af[i] = *reinterpret_cast<const bf16x8_t*>(As + row * ROWB + (((4 * ks + qg) ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+          const int row = wn + 16 * j + r16;
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + row * ROWB + (((4 * ks + qg) ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+          for (int j = 0; j < AN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
+    } else {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int row = wn + 32 * j + r32;
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + row * ROWB + (((2 * ks + h) ^ swz(row)) << 4));
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = arow + wm + 32 * i + r32;
+          af[i] = *reinterpret_cast<const bf16x8_t*>(As + row * ROWB + (((2 * ks + h) ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn + 32 * j + r32;
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + row * ROWB + (((2 * ks + h) ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
   if constexpr (WIN) {
@@ -457,10 +492,10 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
   const OutT* R2 = reinterpret_cast<const OutT*>(p.r2);
   if (R1) R1 += (int64_t)b * p.syb;
   if (R2) R2 += (int64_t)b * p.syb;
-  float bn[FN];
+  float bn[AN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn + 32 * j + r32;
+  for (int j = 0; j < AN; ++j) {
+    const int n = n0 + wn + (M16 ? 16 * j + r16 : 32 * j + r32);
     bn[j] = 0.f;
     if (n < p.Cout) {
       if (p.bias) bn[j] = p.bias[n];
@@ -471,14 +506,27 @@ __global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
   constexpr int CPR = WN / V;            // chunks per staged row
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
+    if constexpr (M16) {  // 32-row band i = 16-row blocks 2i, 2i+1; C/D: row 4*(lane>>4) + reg, col lane&15
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+      for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = acc[i][j][r] + bn[j];
-        if (p.gelu) v = p.gelu == 2 ? v / (1.f + __expf(-v)) : gelu_tanh(v);
-        stg[((r & 3) + 8 * (r >> 2) + 4 * h) * EP + 32 * j + r32] = v;
-      }
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[2 * i + i2][j][r] + bn[j];
+            if (p.gelu) v = p.gelu == 2 ? v / (1.f + __expf(-v)) : gelu_tanh(v);
+            stg[(16 * i2 + 4 * qg + r) * EP + 16 * j + r16] = v;
+          }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[i][j][r] + bn[j];
+          if (p.gelu) v = p.gelu == 2 ? v / (1.f + __expf(-v)) : gelu_tanh(v);
+          stg[((r & 3) + 8 * (r >> 2) + 4 * h) * EP + 32 * j + r32] = v;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < 32 * CPR / 64; ++k) {
       const int c = lane + 64 * k, row = c / CPR, col = (c - row * CPR) * V;

@@ -14,6 +14,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/p
 cp "$(find /tmp/prof -name '*kernel_stats.csv' | head -n 1)" gpurun_out/kernel_stats_$TAG.csv
 # 4 batches under the profiler: warmup 1 + timed 2 + bench.py's instrumented vocoder step 1
 python3 profiles/summarize.py gpurun_out/kernel_stats_$TAG.csv 4 > gpurun_out/kernel_stats_$TAG.txt
+python3 profiles/copy_trace.py "$(find /tmp/prof -name '*kernel_trace.csv' | head -n 1)" > gpurun_out/copy_trace_$TAG.txt || true
 if [ "${2:-pmc}" = "pmc" ]; then
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pmc_df -o run -- python3 profiles/pmc_decode.py > gpurun_out/pmc_df.log 2>&1
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pmc_dw -o run -- python3 profiles/pmc_decode.py > gpurun_out/pmc_dw.log 2>&1
