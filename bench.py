@@ -36,8 +36,8 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 # PMC traffic summaries of the CURRENT build (profiles/run_profiles.sh; FETCH_SIZE x2 per
 # MI355X_MICROARCH.md, calibrated by profiles/pmc_calibrate.py); None when not yet measured
-TRAFFIC_DECODE = "traffic_decode_r03.json"
-TRAFFIC_VOCODER = "traffic_vocoder_r03.json"
+TRAFFIC_DECODE = "traffic_decode_r03s.json"
+TRAFFIC_VOCODER = "traffic_vocoder_r03s.json"
 
 
 class KernelTimer:
