@@ -24,15 +24,27 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 }
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
 
-// Storage-type traits: every kernel computes in f32 and loads/stores T.
+// Storage-type traits: every kernel computes in f32 and loads/stores T.  ITTS_NT_STORE=1 (A/B build):
+// non-temporal stores everywhere St<> is used and at the decode kernels' explicit stores.
+#ifndef ITTS_NT_STORE
+#define ITTS_NT_STORE 0
+#endif
+template <typename T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+#if ITTS_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 template <typename T> struct St;
 template <> struct St<float> {
   __device__ __forceinline__ static float ld(const float* p) { return *p; }
-  __device__ __forceinline__ static void st(float* p, float v) { *p = v; }
+  __device__ __forceinline__ static void st(float* p, float v) { st_out(p, v); }
 };
 template <> struct St<uint16_t> {
   __device__ __forceinline__ static float ld(const uint16_t* p) { return bf2f(*p); }
-  __device__ __forceinline__ static void st(uint16_t* p, float v) { *p = f2bf(v); }
+  __device__ __forceinline__ static void st(uint16_t* p, float v) { st_out(p, f2bf(v)); }
 };
 // IEEE half (the reference activation op also dispatches Half: type_shim.h:20-43); round to nearest even
 template <> struct St<_Float16> {

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm_kernel(DgArgs p) {
       const int n = nt * 32 + (l & 31);
       if (row >= p.M || n >= p.N) continue;
       if (EPI == 2) {  // split-K partial (no bias); reduced in fixed order by itts_residual_reduce_ln
-        reinterpret_cast<float*>(p.y)[ks * p.split_stride + (int64_t)row * p.ldy + n] = tv[k];
+        st_out(reinterpret_cast<float*>(p.y) + ks * p.split_stride + (int64_t)row * p.ldy + n, tv[k]);
         continue;
       }
       float v = tv[k];
@@ -484,8 +484,8 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
       if constexpr (EPI == 1) {
         float* X = reinterpret_cast<float*>(p.y) + (int64_t)row * p.ldy + n;
         const float xv = *X + v;
-        *X = xv;
-        p.xh[(int64_t)row * p.ldxh + n] = f2bf(xv);
+        st_out(X, xv);
+        st_out(p.xh + (int64_t)row * p.ldxh + n, f2bf(xv));
       } else {
         if (p.gelu) v = gelu_tanh_d(v);
         St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);

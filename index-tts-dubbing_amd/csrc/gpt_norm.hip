@@ -134,7 +134,7 @@ __global__ __launch_bounds__(1024) void residual_reduce_ln_v4_kernel(
       if (s < nsplit) p += pv[s][i];
     v[i] = acc[i] + p;
   }
-  *reinterpret_cast<f32x4_t*>(xr) = f32x4_t{v[0], v[1], v[2], v[3]};
+  st_out(reinterpret_cast<f32x4_t*>(xr), f32x4_t{v[0], v[1], v[2], v[3]});
   if (!g1) {  // no LayerNorm (folded into the consumer GEMM): h = x, rounded
     if (h) {
       TO* hr = h + (int64_t)m * ldh + e;
