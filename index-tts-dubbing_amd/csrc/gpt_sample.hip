@@ -64,14 +64,16 @@ __device__ __forceinline__ float uniform01(uint64_t key) { return ((float)(mix64
 // record the chosen token, then write x = mel_emb[tok] + mel_pos[col + pos_delta] and h = ln_1(x)
 // (h = x when g is null: ln_1 is folded into the c_attn GEMM)
 template <typename TH>
+// was_done: done[b] as loaded at the kernel's start (only this row's workgroup writes it, at the end),
+// so the commit does not wait on a global load after the argmax
 __device__ __forceinline__ void commit_and_embed(int b, int ii, int col, int V, int stop, uint8_t* sr, uint8_t* done,
-                                                 int32_t* codes, int64_t ldc, const int32_t* forced,
+                                                 bool was_done, int32_t* codes, int64_t ldc, const int32_t* forced,
                                                  const float* emb, const float* pos_emb, int pos_delta, int D,
                                                  const float* g, const float* bta, float* x, TH* h, int* tok_s,
                                                  float* rv) {
   if (threadIdx.x == 0) {
     if (ii < 0 || ii >= V) ii = stop;  // all -inf / NaN row: behave like a finished row
-    int tok = done[b] ? stop : ii;
+    int tok = was_done ? stop : ii;
     codes[(int64_t)b * ldc + col] = tok;
     if (forced) tok = forced[(int64_t)b * ldc + col];  // teacher forcing: record choice, feed given id
     sr[tok] = 1;
@@ -162,6 +164,7 @@ __global__ __launch_bounds__(kT) void sample_embed_kernel(SampleArgs p) {
   __shared__ int ri[kT / 64];
   __shared__ int tok_s;
   const int b = blockIdx.x;
+  const bool was_done = p.done[b] != 0;
   const int col = p.tstate[0] + p.col_delta;
   const float* lr = p.logits + (int64_t)b * p.ldl;
   uint8_t* sr = p.seen + (int64_t)b * p.ldl;
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(kT) void sample_embed_kernel(SampleArgs p) {
     }
   }
   block_argmax(best, bi, rv, ri);
-  commit_and_embed<TH>(b, bi, col, p.V, p.stop, sr, p.done, p.codes, p.ldc, p.forced, p.emb, p.pos_emb,
+  commit_and_embed<TH>(b, bi, col, p.V, p.stop, sr, p.done, was_done, p.codes, p.ldc, p.forced, p.emb, p.pos_emb,
                        p.pos_delta, p.D, p.g, p.bta, p.x, reinterpret_cast<TH*>(p.h), &tok_s, rv);
 }
 
@@ -272,6 +275,7 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
   __shared__ int hist[256], bc[2];  // general warper thresholds (select.h)
   __shared__ int tok_s;
   const int b = blockIdx.x;
+  const bool was_done = p.done[b] != 0;
   const int col = p.tstate[0] + p.col_delta;
   const uint64_t seed = (uint64_t)(uint32_t)p.tstate[2] | ((uint64_t)(uint32_t)p.tstate[3] << 32);
   const uint64_t row = (uint64_t)(uint32_t)(b + p.tstate[1]);  // tstate[1]: global index of row 0
@@ -418,7 +422,7 @@ __global__ __launch_bounds__(kT) void sample_topk_embed_kernel(SampleArgs p) {
     __syncthreads();
     bi = ri[0];
   }
-  commit_and_embed<TH>(b, bi, col, p.V, p.stop, sr, p.done, p.codes, p.ldc, p.forced, p.emb, p.pos_emb,
+  commit_and_embed<TH>(b, bi, col, p.V, p.stop, sr, p.done, was_done, p.codes, p.ldc, p.forced, p.emb, p.pos_emb,
                        p.pos_delta, p.D, p.g, p.bta, p.x, reinterpret_cast<TH*>(p.h), &tok_s, rv);
 }
 
