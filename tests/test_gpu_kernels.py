@@ -253,6 +253,43 @@ def test_attn_decode_matches_torch(S, cache, nsplit):
     assert torch.equal(kd[:, :, keep].cpu(), kc[:, :, keep]) and torch.equal(vd[:, :, keep].cpu(), vc[:, :, keep])
 
 
+def test_attn_decode_ignores_padding_and_future_cache_slots():
+    """Cache slots that are not keys of the row (left padding before pad[b], slots after this step's
+    key) may hold anything, NaN included (torch.empty caches): the output stays finite and equal to
+    the reference over the row's own keys."""
+    _hip, lib = _lib()
+    torch.manual_seed(11)
+    B, H, S, smax = 4, 16, 400, 480
+    D = 64 * H
+    kc = (torch.randn(B, H, smax, 64) * 0.5).to(torch.bfloat16)
+    vc = torch.randn(B, H, smax, 64).to(torch.bfloat16)
+    pad = torch.tensor([0, 5, 40, 1], dtype=torch.int32)
+    kidx = S - 1
+    for b in range(B):
+        kc[b, :, : int(pad[b])] = float("nan")
+        vc[b, :, : int(pad[b])] = float("nan")
+    kc[:, :, kidx + 1:] = float("nan")
+    vc[:, :, kidx + 1:] = float("inf")
+    qkv = torch.randn(B, 3 * D)
+    kd, vd, qd, pd = kc.clone().cuda(), vc.clone().cuda(), qkv.cuda(), pad.cuda()
+    out = torch.zeros(B, D, dtype=torch.bfloat16).cuda()
+    tst = torch.tensor([2, 0, 0, 0], dtype=torch.int32).cuda()
+    _hip.check(lib.itts_attn_decode(qd.data_ptr(), 3 * D, 1, B * 3 * D, None, kd.data_ptr(), vd.data_ptr(),
+                                    kd.stride(0), kd.stride(1), smax, pd.data_ptr(), kidx - 2, tst.data_ptr(),
+                                    out.data_ptr(), D, B, H, _hip.BF16, _hip.BF16, _hip.stream_ptr()), "attn_decode")
+    torch.cuda.synchronize()
+    q = qkv[:, :D].view(B, H, 64)
+    kr, vr = kc.float().clone(), vc.float().clone()
+    kr[:, :, kidx], vr[:, :, kidx] = qkv[:, D:2 * D].view(B, H, 64), qkv[:, 2 * D:].view(B, H, 64)
+    got = out.float().cpu().view(B, H, 64)
+    assert bool(torch.isfinite(got).all())
+    for b in range(B):
+        p0 = int(pad[b])
+        sc = torch.einsum("hd,hsd->hs", q[b], kr[b, :, p0:kidx + 1]) / 8.0
+        ref = torch.einsum("hs,hsd->hd", sc.softmax(-1), vr[b, :, p0:kidx + 1])
+        assert float((got[b] - ref).abs().max()) <= 2e-2 * max(1.0, float(ref.abs().max()))
+
+
 @pytest.mark.parametrize("S,rows", [(37, False), (300, False), (513, True)])
 def test_attn_decode_proj_matches_torch(S, rows):
     """Attention with attn.c_proj fused (itts_attn_decode_proj): part[h][b] = o_h[b] @ W[64h : 64h+64]
