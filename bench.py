@@ -223,6 +223,9 @@ def main():
                     help="greedy (the headline) or beam3: the reference's default production decoding "
                          "(do_sample=True, num_beams=3, top_k=30, top_p=0.8, infer.py:535-543), 3 beam rows "
                          "per utterance (96-row decode step at batch 32)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group (RCCL) even at one rank, so the C4 gather of finished "
+                         "int16 waveforms to rank 0 runs inside every timed step at N = 1 too")
     ap.add_argument("--pipeline", action="store_true",
                     help="run the K timed batches through BatchedTTS.synthesize_many (decode of batch i+1 "
                          "overlapped with the latent pass + vocoder of batch i)")
@@ -236,12 +239,15 @@ def main():
     local = int(os.environ.get("ITTS_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
         backend = os.environ.get("ITTS_DIST_BACKEND", "nccl")
+        init = {} if world > 1 else dict(init_method=f"tcp://127.0.0.1:{os.environ.get('MASTER_PORT', '29511')}",
+                                          world_size=1, rank=0)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, **init)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **init)
 
     from indextts.pipeline import BatchedTTS, SR
     from indextts.sharding import gather_waveforms, shard
@@ -271,7 +277,7 @@ def main():
 
     def step():
         pcm, lens, _ = tts.synthesize(mels, texts, max_mel_tokens=N, min_new_tokens=N, **dec_kw)
-        if world > 1:  # the one collective: finished int16 waveforms to rank 0, in utterance order
+        if use_dist:  # the one collective: finished int16 waveforms to rank 0, in utterance order
             gather_waveforms([pcm[b, : int(lens[b])] for b in range(B)], B * world, dev)
         return float(lens.sum()) / SR
 
@@ -289,7 +295,7 @@ def main():
         res = tts.synthesize_many([(mels, texts)] * args.steps, max_mel_tokens=N, min_new_tokens=N, **dec_kw)
         torch.cuda.synchronize()
         for pcm, lens, _ in res:
-            if world > 1:
+            if use_dist:
                 gather_waveforms([pcm[b, : int(lens[b])] for b in range(B)], B * world, dev)
             audio += float(lens.sum()) / SR
     else:
@@ -378,14 +384,16 @@ def main():
                                f"{'s' if B > 1 else ''} per GPU (one prompt each), L={L} text ids, "
                                f"{N} codes each (EOS suppressed): conditioning+ECAPA, GPT prefill+decode (hipGraph), "
                                "latent pass, BigVGAN2 -> int16" + (", pipelined batches" if args.pipeline else ""),
-                   "global_batch": B * world, "seq_len": N, "parallelism": f"dp{world}"},
+                   "global_batch": B * world, "seq_len": N, "parallelism": f"dp{world}",
+                   "collective": (f"{dist.get_backend()} gather of finished int16 waveforms to rank 0 in every "
+                                  "timed step") if use_dist else None},
         "roofline": dec,
         "roofline_vocoder_conv": voc,
         **hbm,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

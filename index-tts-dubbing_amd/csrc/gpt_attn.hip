@@ -42,8 +42,8 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 
 // One workgroup of NT threads per (head, sequence): NT/8 groups of 8 lanes, group g owns keys
 // g, g + NT/8, ...; lane d8 holds dims 8*d8 .. 8*d8+7.  Issue order: this step's q/k/v, then the
-// round's cached K rows, then its V rows (KB keys per group kept packed in registers: 320 keys per
-// round at NT = 256, KB = 10), so the scores start as soon as K has landed while V still streams;
+// round's cached K rows, then its V rows (KB keys per group kept packed in registers: 384 keys per
+// round at NT = 256, KB = 12), so the scores start as soon as K has landed while V still streams;
 // later rounds are requested while the current one computes.  Scores via 8-lane DPP sums, an online
 // softmax per group (running max m, sum l, partial output o); the groups merge through LDS with all
 // NT threads.  (Measured alternatives, slower at B=32, S~283: 512-thread workgroups; 16 packed keys
@@ -54,8 +54,9 @@ constexpr int kMaxKeys = 1 << 20;  // positions are int32; the cache capacity is
 // share their common prefix, HF's per-step cache reorder becomes this lineage table); this step's
 // key/value go to the sequence's own row b.
 #ifndef ITTS_ATTN_KB
-#define ITTS_ATTN_KB 10
+#define ITTS_ATTN_KB 12
 #endif
+constexpr int kSub = 4;  // keys per group per online-softmax update (every KB is a multiple of it)
 #ifndef ITTS_ATTN_WPS
 #define ITTS_ATTN_WPS 1
 #endif
@@ -200,13 +201,16 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
   };
   // (4) online softmax per 8-lane group over rounds of NG*KB keys.  Software-pipelined: the next
   // round's K rows are requested as soon as this round's scores no longer need kr, its V rows once
-  // this round's P.V is done.
+  // this round's P.V is done.  The softmax itself advances in fixed chunks of kSub keys per group
+  // whatever KB is (KB only sets how far the loads run ahead), so the rounding of a row's result does
+  // not depend on the KB the launcher picked for its batch size: a row decodes bit-identically alone
+  // and inside a 128-row long-form chunk.
+  static_assert(KB % kSub == 0, "keys per round must be a multiple of the softmax chunk");
   float m = -INFINITY, l = 0.f;
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nk; j0 += NG * KB) {
     const bool more = j0 + NG * KB < nk;
     float s[KB];
-    float bm = -INFINITY;
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
       const int j = j0 + NG * u + g;
@@ -221,17 +225,21 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
       for (int e = 0; e < 8; ++e) pt = fmaf(q[e], kx[e], pt);
       pt = sum8_dpp(pt);
       s[u] = j < nk ? pt : -INFINITY;
-      bm = fmaxf(bm, s[u]);
     }
     if (more) kv_load(kr, Kc, j0 + NG * KB);
-    if (bm != -INFINITY) {  // else this group has no valid key in the round
+#pragma unroll
+    for (int c0 = 0; c0 < KB; c0 += kSub) {
+      float bm = -INFINITY;
+#pragma unroll
+      for (int u = c0; u < c0 + kSub; ++u) bm = fmaxf(bm, s[u]);
+      if (bm == -INFINITY) continue;  // this group has no valid key in the chunk
       const float mn = fmaxf(m, bm);
       const float corr = __expf(m - mn);  // m = -inf -> 0
       l *= corr;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] *= corr;
 #pragma unroll
-      for (int u = 0; u < KB; ++u) {
+      for (int u = c0; u < c0 + kSub; ++u) {
         const int j = j0 + NG * u + g;
         const float pr = __expf(s[u] - mn);
         l += pr;
@@ -581,7 +589,9 @@ int attn_decode_launch(const char* fn, const float* qkv, int64_t ldqkv, int nspl
   dim3 grid(H, B);
   hipStream_t s = itts::as_stream(stream);
   const uint16_t* wp = static_cast<const uint16_t*>(wproj);
-  // keys per group per round: 10 (320 keys per workgroup round) for the 32-row steps, 4 for steps of
+  // keys per group per round (the load depth only: the softmax runs in kSub-key chunks whatever KB is,
+  // so the choice below never changes a result bit): 12 (384 keys per workgroup round) for the 32-row
+  // steps (round 3 measured 10; KB must now be a multiple of kSub), 4 for steps of
   // >= 128 rows (long-form chunks), whose 2048+ workgroups are occupancy-bound at 10 -- B = 128: S = 71
   // 23.8 -> 15.5 us, S = 300 31.1 vs 31.7 (profiles/ubench_attn_kb_r03.txt) -- and for the beam
   // lineage form at any row count: its beams re-read a shared prefix out of L2, so 4 workgroups per CU

@@ -121,6 +121,12 @@ extern "C" int itts_gpt_prefill(const ItTsGptSeqWeights* ws, const ItTsGptWeight
                "decode and sequence weights disagree");
   ITTS_REQUIRE(s >= 1 && s + 1 <= st->max_kv, fn, "prompt longer than the KV capacity");
   ITTS_REQUIRE(smp->mode >= 0 && smp->mode <= 2, fn, "sampling mode must be 0, 1 or 2");
+  // the decode steps read key kv_base + t: the prompt block fills keys 0 .. s, so the first decode key is s + 1
+  ITTS_REQUIRE(st->kv_base == s + 1, fn, "state kv_base must equal s + 1 (the prompt block's length)");
+  ITTS_REQUIRE(ws->dtype == ITTS_F32 || w->head_w, fn, "bf16 mode needs head_w (mel_head, 32-column fragments)");
+  ITTS_REQUIRE(st->xh && st->logits && st->k_cache && st->v_cache && st->tstate, fn, "null state buffer");
+  ITTS_REQUIRE(smp->mode == 2 || (st->seen && st->done && st->codes && st->x && w->mel_emb && w->mel_pos), fn,
+               "sampler state missing (seen / done / codes / x / mel embeddings)");
   const int R = st->rows, D = w->d_model, H = w->n_head;
   const int64_t cache_hs = (int64_t)st->max_kv * kHD, cache_bs = (int64_t)H * cache_hs;
   const int64_t M = (int64_t)R * (s + 1);

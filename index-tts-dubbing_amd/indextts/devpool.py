@@ -10,7 +10,12 @@ cue lookahead (``IndexTTS.prefetch``) deals the upcoming cues over the parent's 
 workers (longest first onto the least-loaded device), waits for every share and files the results
 per cue, so ``infer`` returns each cue's PCM in the caller's order exactly as before.  Rows never
 interact inside the batched pipeline, so a cue's int16 PCM does not depend on which device or batch
-produced it (deterministic decoding: bit for bit, tests/test_gpu_devpool.py).
+produced it (deterministic decoding: bit for bit; ``tests/test_gpu_longform.py::
+test_two_engines_one_gpu_equal_per_call`` checks it with two processes on ONE GPU and short rows).
+
+A worker that does not answer within ``ITTS_WORKER_TIMEOUT`` seconds (default 600 per request,
+1800 to load), or answers out of step (a reply for another request id), is terminated and marked
+dead; the caller redoes its share locally (``IndexTTS._infer_many_devices``).
 
 Utterances shard with no data-path collective: what crosses processes is the finished int16 PCM
 (pickled through the pipe), as the north star's "only a gather of finished waveforms".  The
@@ -93,6 +98,8 @@ class DevicePool:
                  builder: str = "indextts.infer:IndexTTS"):
         ctx = mp.get_context("spawn")
         self.devices = list(devices)
+        self.request_timeout = float(os.environ.get("ITTS_WORKER_TIMEOUT", "600"))
+        self.init_timeout = max(self.request_timeout, 1800.0)
         self._conns, self._procs, self._ready = [], [], []
         self._rid = itertools.count()
         for d in self.devices:
@@ -108,15 +115,32 @@ class DevicePool:
     def __len__(self):
         return len(self.devices)
 
+    def _kill(self, i: int):
+        """Mark worker i dead and stop its process (a hung or out-of-step worker is never reused)."""
+        self._ready[i] = False
+        p = self._procs[i]
+        if p.is_alive():
+            p.terminate()
+            p.join(timeout=10)
+
+    def _recv(self, i: int, timeout: float):
+        """conn.recv() bounded by ``timeout`` seconds; a timeout kills the worker."""
+        conn = self._conns[i]
+        if not conn.poll(timeout):
+            self._kill(i)
+            raise WorkerError(f"worker {self.devices[i]}: no reply within {timeout:.0f} s")
+        return conn.recv()
+
     def _wait_ready(self, i: int) -> bool:
         if self._ready[i] is None:
             try:
-                tag, status, info = self._conns[i].recv()
+                tag, status, info = self._recv(i, self.init_timeout)
                 self._ready[i] = tag == "init" and status == "ok"
                 if not self._ready[i]:
                     print(f">> IndexTTS worker on {self.devices[i]} failed to start:\n{info}")
-            except (EOFError, OSError):
-                self._ready[i] = False
+                    self._kill(i)
+            except (EOFError, OSError, WorkerError):
+                self._kill(i)
         return bool(self._ready[i])
 
     def alive(self) -> List[int]:
@@ -134,11 +158,12 @@ class DevicePool:
     def result(self, ticket: Tuple[int, int]):
         i, rid = ticket
         try:
-            got, status, payload = self._conns[i].recv()
+            got, status, payload = self._recv(i, self.request_timeout)
         except (EOFError, OSError) as e:
-            self._ready[i] = False
+            self._kill(i)
             raise WorkerError(f"worker {self.devices[i]} died: {e}") from e
-        if got != rid:
+        if got != rid:  # the pipe is out of step (e.g. an interrupted earlier request): never reuse it
+            self._kill(i)
             raise WorkerError(f"worker {self.devices[i]}: reply {got} for request {rid}")
         if status != "ok":
             raise WorkerError(f"worker {self.devices[i]}: {payload}")

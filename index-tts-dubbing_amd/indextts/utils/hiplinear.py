@@ -128,8 +128,9 @@ class HipLinearBank:
         if a.stride(0) != K or a.stride(1) != 1:
             a = a.contiguous()
         M = a.shape[0]
-        tiles = -(-M // 256) * -(-N // 256)
-        ns = next((n for n in (8, 4, 2) if K % (64 * n) == 0 and K // n >= 1024 and tiles * n <= 1024), 1)
+        # the split count depends on K only (never on M, the rows of every prompt in the batch), so each
+        # output's reduction order -- and a prompt's conditioning -- is the same in any batch
+        ns = next((n for n in (8, 4, 2) if K % (64 * n) == 0 and K // n >= 1024), 1)
         if ns == 1 or N % 4:
             return self(x, name)
         ent = self._packed.get((name, ns))

@@ -356,8 +356,11 @@ class HipBigVGAN:
         return wav, pcm
 
     @torch.no_grad()
-    def _forward_py(self, latent: torch.Tensor, lengths: torch.Tensor, spk: torch.Tensor, want_pcm: bool = True):
-        """The same launches from Python (reference for tests/test_gpu_vocoder.py's C-ABI test)."""
+    def _forward_py(self, latent: torch.Tensor, lengths: torch.Tensor, spk: torch.Tensor, want_pcm: bool = True,
+                    taps: dict = None):
+        """The same launches from Python (reference for tests/test_gpu_vocoder.py's C-ABI test).
+        ``taps`` (tests): filled with copies of the stage boundaries, channel-last bf16 --
+        "pre" (conv_pre + cond), "stage{i}" (after upsampling stage i), and the matching lengths."""
         dev = self.device
         x = latent.to(dev)
         if x.dtype != torch.bfloat16:
@@ -370,6 +373,8 @@ class HipBigVGAN:
         C0 = self.conv_pre.cout
         cur_in = self._buf("xs_a", (B, T, C0))
         self._conv(self.conv_pre, x, cur_in, lens, bias_b=pre_b)
+        if taps is not None:
+            taps["pre"], taps["pre_lens"] = cur_in.clone(), lens.clone()
         Tcur = T
         for i, (u, convs, C) in enumerate(self.ups):
             Tn = Tcur * u
@@ -410,6 +415,8 @@ class HipBigVGAN:
                         self._conv(c2, t1, dst, lens_n, r1=src, r2=r2, alpha=alpha)
                     src = dst
             cur_in, Tcur, lens = xs, Tn, lens_n
+            if taps is not None:
+                taps[f"stage{i}"], taps[f"stage{i}_lens"] = xs.clone(), lens_n.clone()
         t1 = self._buf("t1", cur_in.shape)
         self._act(self.act_post, cur_in, t1, lens)
         wav = torch.empty(B, Tcur, dtype=torch.float32, device=dev)

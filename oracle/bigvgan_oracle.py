@@ -85,25 +85,36 @@ class BigVGANOracle:
             x = xt + x
         return x
 
-    def forward(self, latent, spk):
-        """latent [B, T, gpt_dim], spk [B, spk_dim] -> wav [B, 1, T * prod(upsample_rates)] float32."""
-        sd, h = self.sd, self.h
-        s = spk.float()[:, :, None]
+    def pre(self, latent, spk):
+        """conv_pre + cond_layer (models.py:220-226): latent [B, T, gpt_dim] -> [B, C0, T]."""
+        sd = self.sd
         x = self.conv("conv_pre", latent.float().transpose(1, 2))
-        x = x + F.conv1d(s, sd["cond_layer.weight"], sd["cond_layer.bias"])
+        return x + F.conv1d(spk.float()[:, :, None], sd["cond_layer.weight"], sd["cond_layer.bias"])
+
+    def stage(self, i, x, spk):
+        """upsampling stage i (models.py:228-243): ups[i] + conds[i], then the mean of the AMP blocks."""
+        sd, h = self.sd, self.h
+        u, k = int(h.upsample_rates[i]), int(h.upsample_kernel_sizes[i])
+        x = F.conv_transpose1d(x, sd[f"ups.{i}.0.weight"], sd[f"ups.{i}.0.bias"], stride=u, padding=(k - u) // 2)
+        x = x + F.conv1d(spk.float()[:, :, None], sd[f"conds.{i}.weight"], sd[f"conds.{i}.bias"])
         nk = len(h.resblock_kernel_sizes)
-        for i, (u, k) in enumerate(zip(h.upsample_rates, h.upsample_kernel_sizes)):
-            x = F.conv_transpose1d(x, sd[f"ups.{i}.0.weight"], sd[f"ups.{i}.0.bias"], stride=int(u),
-                                   padding=(int(k) - int(u)) // 2)
-            x = x + F.conv1d(s, sd[f"conds.{i}.weight"], sd[f"conds.{i}.bias"])
-            xs = None
-            for j, (kk, dils) in enumerate(zip(h.resblock_kernel_sizes, h.resblock_dilation_sizes)):
-                r = self.amp_block(i * nk + j, x, int(kk), [int(d) for d in dils])
-                xs = r if xs is None else xs + r
-            x = xs / nk
-        x = self.act("activation_post", x)
-        x = self.conv("conv_post", x)
-        return torch.tanh(x)
+        xs = None
+        for j, (kk, dils) in enumerate(zip(h.resblock_kernel_sizes, h.resblock_dilation_sizes)):
+            r = self.amp_block(i * nk + j, x, int(kk), [int(d) for d in dils])
+            xs = r if xs is None else xs + r
+        return xs / nk
+
+    def post(self, x):
+        """activation_post -> conv_post -> tanh (models.py:246-248)."""
+        return torch.tanh(self.conv("conv_post", self.act("activation_post", x)))
+
+    def forward(self, latent, spk):
+        """latent [B, T, gpt_dim], spk [B, spk_dim] -> wav [B, 1, T * prod(upsample_rates)] float32
+        (BigVGAN.forward, models.py:201-250: pre, the upsampling stages, post)."""
+        x = self.pre(latent, spk)
+        for i in range(len(self.h.upsample_rates)):
+            x = self.stage(i, x, spk)
+        return self.post(x)
 
 
 def to_int16(wav: torch.Tensor) -> torch.Tensor:

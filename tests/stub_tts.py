@@ -59,4 +59,7 @@ class WorkerStub:
         if "__die__" in texts:
             import os
             os._exit(3)
+        if any("__hang__" in t for t in texts):
+            import time
+            time.sleep(3600)
         return [(24000, fake_pcm(t, gen)) for t in texts]

@@ -290,6 +290,37 @@ def test_attn_decode_ignores_padding_and_future_cache_slots():
         assert float((got[b] - ref).abs().max()) <= 2e-2 * max(1.0, float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("S", [300, 700])
+def test_attn_decode_row_bit_identical_alone_and_in_a_128_row_step(S):
+    """The launcher loads 4 keys per group per round for >= 128-row steps (long-form chunks) and 12 for
+    smaller ones; the online softmax advances in fixed 4-key chunks either way, so a row's output does
+    not depend on the batch it was decoded in (S > 128 keys, one row alone vs the same
+    row inside a 128-row step, bit for bit)."""
+    _hip, lib = _lib()
+    B, H, smax = 128, 16, S + 8
+    D = 64 * H
+    g = torch.Generator(device="cuda").manual_seed(S)
+    kc = (torch.randn(B, H, smax, 64, generator=g, device="cuda") * 0.5).to(torch.bfloat16)
+    vc = torch.randn(B, H, smax, 64, generator=g, device="cuda").to(torch.bfloat16)
+    qkv = torch.randn(B, 3 * D, generator=g, device="cuda")
+    pad = (torch.arange(B, device="cuda", dtype=torch.int32) * 7) % 41
+    kv_base, t = S - 1 - 2, 2
+    tst = torch.tensor([t, 0, 0, 0], dtype=torch.int32).cuda()
+
+    def run(rows):
+        kd, vd = kc[:rows].clone(), vc[:rows].clone()
+        out = torch.zeros(rows, D, dtype=torch.bfloat16, device="cuda")
+        _hip.check(lib.itts_attn_decode(qkv.data_ptr(), 3 * D, 1, B * 3 * D, None, kd.data_ptr(), vd.data_ptr(),
+                                        kd.stride(0), kd.stride(1), smax, pad.data_ptr(), kv_base, tst.data_ptr(),
+                                        out.data_ptr(), D, rows, H, _hip.BF16, _hip.BF16, _hip.stream_ptr()),
+                   "attn_decode")
+        torch.cuda.synchronize()
+        return out.cpu()
+
+    full, alone = run(128), run(3)
+    assert torch.equal(full[:3], alone)
+
+
 @pytest.mark.parametrize("S,rows", [(37, False), (300, False), (513, True)])
 def test_attn_decode_proj_matches_torch(S, rows):
     """Attention with attn.c_proj fused (itts_attn_decode_proj): part[h][b] = o_h[b] @ W[64h : 64h+64]

@@ -178,3 +178,30 @@ def test_device_pool_protocol_spawned_workers():
         assert len(pool.alive()) == 1
     finally:
         pool.close()
+
+
+def test_device_pool_hung_and_out_of_step_workers_are_dropped():
+    """a worker that does not answer within the request timeout is terminated and its
+    share redone locally; a reply for another request id (the pipe out of step) kills the worker
+    instead of poisoning every later share."""
+    pool = DevicePool("cfg", "dir", True, ["cuda:1", "cuda:2"], builder="stub_tts:WorkerStub")
+    try:
+        assert pool.alive() == [0, 1]
+        pool.request_timeout = 3.0
+        tts = StubTTS(pool=pool)
+        texts = ["a " * 20, "__hang__ " * 8, "x", "y y"]  # longest first: the hanging cue lands on a worker
+        with pytest.warns(RuntimeWarning, match="no reply"):
+            res = tts._infer_many_devices(PROMPT, texts, 120, {})
+        for t, r in zip(texts, res):
+            np.testing.assert_array_equal(r[1], fake_pcm(t, {}))
+        assert len(pool.alive()) == 1
+        # out of step: request A's reply is never collected, request B then reads A's reply
+        wi = pool.alive()[0]
+        pool.submit(wi, PROMPT, ["a"], 120, {})
+        tb = pool.submit(wi, PROMPT, ["b"], 120, {})
+        from indextts.devpool import WorkerError
+        with pytest.raises(WorkerError, match="reply"):
+            pool.result(tb)
+        assert pool.alive() == []
+    finally:
+        pool.close()
