@@ -35,7 +35,7 @@ int itts_abi_version(void);
 const char* itts_build_target(void); /* "gfx950" */
 /* sizeof of the ABI structs below (0 ItTsGptLayerW, 1 ItTsGptWeights, 2 ItTsGptDecodeState,
  * 3 ItTsSampling, 4 ItTsConv, 5 ItTsAct, 6 ItTsAmpLayer, 7 ItTsBigvganStage, 8 ItTsBigvganWeights,
- * 9 ItTsGptSeqLayerW, 10 ItTsGptSeqWeights),
+ * 9 ItTsGptSeqLayerW, 10 ItTsGptSeqWeights, 11 ItTsGptPlLayerW),
  * -1 otherwise: lets a binding check its struct layouts. */
 int64_t itts_struct_size(int which);
 
@@ -336,6 +336,7 @@ typedef struct ItTsGptLayerW {
   const float* fc_c;
   const void* proj_w;   /* mlp.c_proj, 32-column fragment order */
   const float* proj_b;
+  const void* o_w;      /* attn.c_proj, 32-column fragment order (split-K 8 over head pairs; ABI 3) */
 } ItTsGptLayerW;
 
 /* The UnifiedVoice GPT for decoding (gpt/model.py:255-281,85-192): layers, ln_f + final_norm (Q5),
@@ -428,8 +429,9 @@ int itts_gpt_prefill(const ItTsGptSeqWeights* ws, const ItTsGptWeights* w, const
 
 /* One whole KV-cached decode step (one HF generate iteration of inference_speech, gpt/model.py:655-708),
  * per layer: c_attn with ln_1 folded (itts_decode_gemm16x) -> itts_attn_decode[_rows] -> attn.c_proj
- * (itts_decode_gemm16x residual) -> c_fc with ln_2 folded + gelu -> mlp.c_proj split-K 8
- * (itts_decode_gemm) -> itts_residual_reduce_ln (the last layer's with ln_f + final_norm, Q5); then
+ * split-K 8 over head pairs (itts_decode_gemm) -> itts_residual_reduce_ln -> c_fc with ln_2 folded +
+ * gelu -> mlp.c_proj split-K 8 (itts_decode_gemm) -> itts_residual_reduce_ln (the last layer's with
+ * ln_f + final_norm, Q5); then
  * mel_head, token selection + next embedding (ItTsSampling modes 0/1) and the step advance.  The
  * caller's prefill (itts_attn_prefill + the GEMMs above) fills the cache and the first token; rows
  * padded to whole 32-row tiles in xh / o / f.  Graph-capturable: the step counter lives on the device. */
@@ -441,6 +443,34 @@ int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecodeState* stat
  * Same results as nsteps calls of itts_gpt_decode_step. */
 int itts_gpt_decode_steps(const ItTsGptWeights* w, const ItTsGptDecodeState* state, const ItTsSampling* sampling,
                           int nsteps, void* stream);
+
+/* ---- persistent decode layer (gpt_layer.hip) ----------------------------------------------------
+ * One GPT-2 block of the decode step (HF modeling_gpt2.py:246-306 via gpt/model.py:115-192) as ONE
+ * launch of 256 workgroups (one per CU) joined by in-launch hand-offs, each workgroup's weights
+ * requested at the start of the launch.  IndexTTS-1.5 shapes (d_model 1024, 16 heads) and 1..32 rows,
+ * no beam lineage; bit-identical to the launch chain (itts_gpt_decode_steps).  Extra weights per layer
+ * besides ItTsGptLayerW: */
+typedef struct ItTsGptPlLayerW {
+  const void* qkv_w12;  /* c_attn (ln_1 folded), 12 columns per workgroup: [256][32][4][12][8] bf16 */
+  const float* qkv_uc;  /* [256][2][12]: u and c of those columns (itts_decode_gemm16x fold terms) */
+} ItTsGptPlLayerW;
+/* Bytes of the device scratch the persistent layers share (hand-off buffers, counters and a sticky
+ * error word); zero it once after allocation. */
+int64_t itts_gpt_pl_scratch_bytes(void);
+/* 1 if the persistent path runs this shape on the current device (256 CUs resident at once), else 0. */
+int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows);
+/* Zero the step's hand-off counters (a memset node); once before the layers of every decode step. */
+int itts_gpt_pl_begin_step(void* scratch, void* stream);
+/* Layer `layer` of decode step `kstep` of a multi-step call (key kv_base + t + kstep); `last`: leave
+ * the mlp.c_proj reduce (+ ln_f + final_norm) to itts_residual_reduce_ln over the scratch partials. */
+int itts_gpt_layer_pl(const ItTsGptLayerW* layer_w, const ItTsGptPlLayerW* pl, const ItTsGptDecodeState* state,
+                      int layer, int kstep, int last, void* scratch, void* stream);
+/* A hand-off timeout recorded in the scratch (0 = none; else every later layer launch returns at once
+ * and the results are invalid until the scratch is zeroed again).  Synchronises `stream`. */
+int itts_gpt_pl_error(const void* scratch, void* stream, int* code);
+/* itts_gpt_decode_steps with every layer on the persistent path (pl: [n_layer]). */
+int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPlLayerW* pl, void* scratch,
+                             const ItTsGptDecodeState* state, const ItTsSampling* sampling, int nsteps, void* stream);
 
 #ifdef __cplusplus
 }

@@ -99,6 +99,9 @@ void set_error(const std::string& msg);
 int fail(const char* fn, const char* what);
 int check_launch(const char* fn);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+// mel_head + token selection + next embedding of decode step k (gpt_step.hip)
+int gpt_head_sample(const ItTsGptWeights* w, const ItTsGptDecodeState* st, const ItTsSampling* smp, int k,
+                    void* stream);
 }  // namespace itts
 
 #define ITTS_REQUIRE(cond, fn, what) \

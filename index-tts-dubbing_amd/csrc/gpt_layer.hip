@@ -1,0 +1,752 @@
+// One GPT-2 decode layer as ONE persistent launch (gfx950): the five dependent kernels of the launch
+// chain (gpt_step.hip: c_attn, attention, attn.c_proj + reduce, c_fc, mlp.c_proj + reduce) become the
+// phases of one grid of 256 workgroups (one per CU), joined by in-launch hand-offs, with every weight
+// byte of the layer requested at the START of the launch -- before the dependency edges it would
+// otherwise wait behind (MI355X_MICROARCH.md rows prefetch-credit / engine-vs-launches).
+//
+// Reference op: HF GPT2Block (modeling_gpt2.py:246-306) inside GPT2InferenceModel.forward
+// (gpt/model.py:115-192) for one KV-cached decode step of inference_speech (gpt/model.py:655-708).
+//
+// Geometry (IndexTTS-1.5: D = 1024, 16 heads x 64, F = 4096; rows R <= 32, one 32-row MFMA tile):
+//   workgroup b = 8 j + c: cluster c = b % 8 (round-robin dispatch puts a cluster on one XCD: a speed
+//   assumption only, never a correctness one), index j in the cluster.  Cluster c owns heads 2c, 2c+1,
+//   c_fc columns [512c, 512c+512) and K range [512c, 512c+512) of mlp.c_proj (= split s of the chain's
+//   split-K 8), and k-steps [128c, 128c+128) of attn.c_proj (its split c).  8 waves; right after its
+//   c_attn operands and K/V rows, each wave requests 1/8 of this workgroup's attn.c_proj / c_fc /
+//   mlp.c_proj weights (72 KiB) into LDS by LDS-DMA, so the weights of the later phases stream while
+//   the early phases and their hand-offs run.  (A dedicated 9th loader wave cost 3 waves per SIMD =
+//   168 VGPRs and spilled.)
+//   A  c_attn (ln_1 folded): 12 columns of head h = 2c + j/16 (3072 / 256), A = x^ (previous launch).
+//      The attention waves request their first round of K/V rows BEFORE this phase's MFMAs.
+//   E1 q/k/v -> attention: 8-byte {tag, value} granules (the data is the flag: no drain, so the K/V
+//      loads stay in flight), 16 producers -> the same 16 workgroups.
+//   B  attention of rows 2(j%16), 2(j%16)+1 of head h (4 waves each; the attn_decode_kernel algorithm).
+//   E2 o -> attn.c_proj: write-through stores, drain, one counter per cluster (32 adders).
+//   C  attn.c_proj split c: 32 output columns (tile j), 8 k-steps of 16 (one per wave) -> partial.
+//   E3 partials -> reduce: one counter per column tile j (8 adders, one per cluster).
+//   D  x1 = x + (b_o + sum_c partial_c) for tile j, x1^ -> the cluster's copy of x^ (E4: 32 adders).
+//   E  c_fc (ln_2 folded) + gelu: 16 columns (tile 32c + j), A = the cluster's x1^.
+//   E5 f -> mlp.c_proj: cluster counter (32 adders).
+//   F  mlp.c_proj split c: 32 columns (tile j), 32 k-steps of 16 (4 per wave) -> partial.
+//   E6 partials -> reduce (8 adders per tile); G  x2 = x1 + (b_proj + sum_c partial_c), x, x^ stored.
+// Every phase is the chain kernel's arithmetic in the chain kernel's order (same MFMA shapes, same
+// k-step-to-wave interleave, same fixed-order cross-wave and cross-split sums), so the layer is
+// bit-identical to the launch chain with attn.c_proj as split-K 8 + reduce (gpt_step.hip).
+// Hand-offs (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md visibility table row 1):
+// payload stored sc1 (write-through), every storing wave s_waitcnt vmcnt(0), workgroup barrier, ONE
+// lane adds to the counter (relaxed, agent scope); the consumer polls relaxed with s_sleep, every load
+// of handed-off bytes is an sc1 load.  Every spin is bounded: a timeout sets an error word and the
+// whole grid drains (results then garbage, the host reports the error); counters and granules are
+// zeroed by a memset node before every step.
+#include "common.h"
+
+namespace {
+
+constexpr int kD = 1024, kH = 16, kHD = 64, kF = 4096;
+constexpr int kNC = 8, kCPC = 32, kWG = kNC * kCPC;  // clusters, workgroups per cluster, grid
+constexpr int kNW = 8;                                // compute waves
+constexpr int kThreads = kNW * 64;
+constexpr int kQC = 12;                               // c_attn columns per workgroup
+constexpr int kKB = 8;                                // attention keys per group per round (load depth)
+constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
+constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s), then the grid drains
+
+// scratch layout (bytes); the first kZeroBytes are zeroed before every step
+constexpr int64_t kOffCnt = 0, kCntWords = 128;
+constexpr int64_t kOffGq = 512;                                    // [16 heads][32 rows][192] u64
+constexpr int64_t kOffOb = kOffGq + (int64_t)kH * 32 * 192 * 8;    // [8][32][128] bf16
+constexpr int64_t kOffP1 = kOffOb + (int64_t)kNC * 32 * 128 * 2;   // [8][32][1024] f32
+constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * 32 * kD * 4;    // [8][32][1024] bf16
+constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * 32 * kD * 2;    // [8][32][512] bf16
+constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * 32 * 512 * 2;   // [8][32][1024] f32
+constexpr int64_t kOffErr = kOffP2 + (int64_t)kNC * 32 * kD * 4;  // sticky error word (not zeroed per step)
+constexpr int64_t kScratchBytes = kOffErr + 256;
+constexpr int64_t kZeroBytes = kOffOb;  // counters + granules
+enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56 };
+
+// LDS layout (bytes)
+constexpr int L_WO = 0, L_WFC = L_WO + 8 * 1024, L_WPJ = L_WFC + 32 * 1024, L_RED = L_WPJ + 32 * 1024;
+constexpr int L_STAT = L_RED + 32 * 1024;                      // rsum[8][32], rsq[8][32], mu[32], rs[32]
+constexpr int kPvRows = 32 + 4 + 1, kPvPitch = kHD + 1;
+constexpr int kUnitBytes = (3 * kHD + 2 * 32 + kPvRows * kPvPitch + kHD) * 4;  // qs kn vn gm gl pv ofin
+constexpr int L_ATT = L_STAT + (2 * 8 * 32 + 2 * 32) * 4;
+constexpr int L_OBF = L_ATT + 2 * ((kUnitBytes + 15) / 16 * 16);  // [2][64] bf16 o, then [32][16] bf16 f
+constexpr int L_FLAG = L_OBF + 32 * 16 * 2;
+constexpr int kLdsBytes = L_FLAG + 16;
+
+struct PlArgs {
+  const u32x4_t* qkv_w12;  // [256][32 ks][4 q][12 c] x 16 B
+  const float* qkv_uc;     // [256][2][12]
+  const u32x4_t* o_w;      // attn.c_proj, pack_skinny [32 tiles][64 ks][64][8]
+  const float* o_b;
+  const u32x4_t* fc_w16;   // c_fc (ln_2 folded), pack_skinny16 [256 tiles][32 ks][64][8]
+  const float *fc_u, *fc_c;
+  const u32x4_t* proj_w;   // mlp.c_proj, pack_skinny [32 tiles][256 ks][64][8]
+  const float* proj_b;
+  float* x;                // [R][1024] f32
+  uint16_t* xh;            // [32][1024] bf16 (rows >= R: read, never written)
+  uint16_t *kc, *vc;       // this layer's cache [R][16][max_kv][64]
+  int64_t cache_bs, cache_hs;
+  const int32_t* pad;
+  const int32_t* tstate;
+  int kv_base, kstep, R, layer, last;
+  float eps;
+  unsigned char* scratch;
+};
+
+__device__ __forceinline__ float gelu_tanh_pl(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+// workgroup barrier that waits for this wave's LDS traffic only: a __syncthreads() would also drain
+// every vector-memory load in flight (the K/V rows requested ahead of the c_attn phase)
+__device__ __forceinline__ void bar() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// every storing wave's write-through stores have left (Guideline 16 R1: before the counter add)
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void add_relaxed(uint32_t* p) {
+  __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_u32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane polls `ctr` until >= target (bounded); returns false on timeout / a failed grid
+__device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uint32_t code) {
+  for (uint32_t n = 0;; ++n) {
+    if (ld_relaxed(ctr) >= target) return true;
+    if ((n & 255) == 255 && ld_relaxed(err) != 0) return false;
+    if (n > kSpinMax) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int b = blockIdx.x, c = b % kNC, j = b / kNC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = j >> 4, jj = j & 15, h = 2 * c + hh;
+  const uint32_t L1 = (uint32_t)p.layer + 1;  // epoch: counters / granules grow by one per layer
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(p.scratch + kOffCnt);
+  uint32_t* err = reinterpret_cast<uint32_t*>(p.scratch + kOffErr);
+  // a hand-off of an earlier launch timed out: drain at once (results are invalid; the host reports it)
+  if (ld_relaxed(err) != 0) return;
+  uint64_t* gq = reinterpret_cast<uint64_t*>(p.scratch + kOffGq);
+  unsigned char* ob = p.scratch + kOffOb;
+  float* p1 = reinterpret_cast<float*>(p.scratch + kOffP1);
+  unsigned char* xc = p.scratch + kOffXc;
+  unsigned char* fcb = p.scratch + kOffFc;
+  float* p2 = reinterpret_cast<float*>(p.scratch + kOffP2);
+  float* red = reinterpret_cast<float*>(smem + L_RED);
+  float* rsum = reinterpret_cast<float*>(smem + L_STAT);
+  float* rsq = rsum + 8 * 32;
+  float* mu = rsq + 8 * 32;
+  float* rsd = mu + 32;
+  int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
+  constexpr bool compute = true;  // (every wave computes; kept as a name for the phase guards)
+  const int R = p.R;
+  if (tid == 0) *abort_flag = 0;
+
+  // ---- (A0) compute waves: c_attn operands first (weights nt, 12 of 16 fragment columns real; A = x^
+  // rows 0..31), then the attention's first round of K/V rows, then this tile's residual slice
+  const int w = wave;
+  const int c16 = lane & 15, q4 = lane >> 4;
+  const int kidx = p.kv_base + p.tstate[0] + p.kstep;
+  u32x4_t bw[4] = {}, av[4][2] = {};
+  const int u = w >> 2;                                  // attention unit of this wave (rows 2jj + u)
+  const int r_u = 2 * jj + u;
+  const bool act_u = r_u < R;
+  const int rr = act_u ? r_u : 0;
+  const int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
+  constexpr int NG = 32;
+  const int p0 = p.pad ? p.pad[rr] : 0;
+  const int nk = kidx + 1 - p0;
+  const uint16_t* Kc = p.kc + (int64_t)rr * p.cache_bs + (int64_t)h * p.cache_hs;
+  const uint16_t* Vc = p.vc + (int64_t)rr * p.cache_bs + (int64_t)h * p.cache_hs;
+  u32x4_t kr[kKB], vr[kKB];
+  auto kv_load = [&](u32x4_t (&dst)[kKB], const uint16_t* base, int j0) {
+#pragma unroll
+    for (int uu = 0; uu < kKB; ++uu) {
+      const int jk = min(j0 + NG * uu + g, max(nk - 2, 0));
+      dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(base + (int64_t)(p0 + jk) * kHD + 8 * d8));
+    }
+  };
+  const int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns
+  float2 x_old = {0.f, 0.f};
+  if (compute) {
+    const u32x4_t* wq = p.qkv_w12 + (int64_t)b * 32 * 4 * kQC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = w + 8 * i;
+      bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    kv_load(kr, Kc, 0);
+    kv_load(vr, Vc, 0);
+    const int xr = xrow < R ? xrow : R - 1;
+    const float2 xv = *reinterpret_cast<const float2*>(p.x + (int64_t)xr * kD + xcol);
+    x_old = xrow < R ? xv : float2{0.f, 0.f};
+    __builtin_amdgcn_sched_barrier(0);
+    // this workgroup's attn.c_proj (8 KiB), c_fc (32 KiB), mlp.c_proj (32 KiB) weight slices, global ->
+    // LDS by DMA (1 KiB per wave instruction, lane-linear = fragment order, nt), instruction t by wave t % 8
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+      const int t = w + 8 * m;
+      const u32x4_t* src;
+      int dst;
+      if (t < 8) {
+        src = p.o_w + (((int64_t)j * 64 + 8 * c + t) * 64 + lane);
+        dst = L_WO + t * 1024;
+      } else if (t < 40) {
+        src = p.fc_w16 + (((int64_t)(32 * c + j) * 32 + (t - 8)) * 64 + lane);
+        dst = L_WFC + (t - 8) * 1024;
+      } else {
+        src = p.proj_w + (((int64_t)j * 256 + 32 * c + (t - 40)) * 64 + lane);
+        dst = L_WPJ + (t - 40) * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(smem + dst), 16, 0, 2);
+    }
+  }
+
+  // ---- (A) c_attn: decode_gemm16x FOLD arithmetic (k-steps w + 8i, row statistics from the A fragments)
+  f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+  if (compute) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&bw[i]);
+      const bf16x8_t bz = c16 < kQC ? bfr : bf16x8_t{};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&av[i][t]);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = (float)a[e];
+          ssum[t] += v;
+          ssq[t] = fmaf(v, v, ssq[t]);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float a = ssum[t], s2 = ssq[t];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (q4 == 0) {
+        rsum[w * 32 + 16 * t + c16] = a;
+        rsq[w * 32 + 16 * t + c16] = s2;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(w * 8 + 4 * t + r) * 64 + lane] = acc[t][r];
+    }
+  }
+  bar();
+  if (tid < 32) {
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kNW; ++ww) {
+      S += rsum[ww * 32 + tid];
+      Q += rsq[ww * 32 + tid];
+    }
+    const float inv = 1.0f / kD, m = S * inv;
+    mu[tid] = m;
+    rsd[tid] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
+  }
+  bar();
+  if (compute) {  // one output per thread: 32 rows x 16 fragment columns (12 real)
+    const int e = tid >> 6, l = lane, col = l & 15;
+    if (col < kQC) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
+      const int row = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
+      const float* uc = p.qkv_uc + (int64_t)b * 2 * kQC;
+      v = rsd[row] * (v - mu[row] * uc[col]);
+      v += uc[kQC + col];
+      const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
+      const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
+      __hip_atomic_store(gq + ((int64_t)h * 32 + row) * 192 + i, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (i >= kHD && row < R) {  // this step's key / value into the cache (attention kernel: 0 + v, rounded)
+        uint16_t* dst = (i < 2 * kHD ? p.kc : p.vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
+                        (int64_t)kidx * kHD + (i & (kHD - 1));
+        *dst = f2bf(0.f + v);
+      }
+    }
+  }
+
+  // ---- (E1 + B) attention, unit u = rows 2jj + u of head h, waves 4u .. 4u+3
+  unsigned char* ub = smem + L_ATT + u * ((kUnitBytes + 15) / 16 * 16);
+  float* qs = reinterpret_cast<float*>(ub);
+  float* kn = qs + kHD;
+  float* vn = kn + kHD;
+  float* gm = vn + kHD;
+  float* gl = gm + 32;
+  float* pv = gl + 32;
+  float* ofin = pv + kPvRows * kPvPitch;
+  if (compute && (w & 3) == 0 && act_u) {  // the unit's first wave sweeps its 192 granules
+    const uint64_t* src = gq + ((int64_t)h * 32 + r_u) * 192;
+    uint64_t g0, g1, g2;
+    bool ok = false;
+    for (uint32_t n = 0;; ++n) {
+      g0 = ld_sc1_u64(src + lane);
+      g1 = ld_sc1_u64(src + 64 + lane);
+      g2 = ld_sc1_u64(src + 128 + lane);
+      const bool mine = (uint32_t)(g0 >> 32) == L1 && (uint32_t)(g1 >> 32) == L1 && (uint32_t)(g2 >> 32) == L1;
+      if (__all(mine)) {
+        ok = true;
+        break;
+      }
+      if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err) != 0)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) {
+      if (lane == 0) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *abort_flag = 1;
+      }
+    } else {
+      qs[lane] = (0.f + __uint_as_float((uint32_t)g0)) * 0.125f;  // 1/sqrt(64), exact
+      kn[lane] = 0.f + __uint_as_float((uint32_t)g1);
+      vn[lane] = 0.f + __uint_as_float((uint32_t)g2);
+    }
+  }
+  bar();
+  if (*abort_flag) return;
+  float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  if (compute && act_u) {
+    float q[8], kme[8], vme[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      q[e] = qs[8 * d8 + e];
+      kme[e] = kn[8 * d8 + e];
+      vme[e] = vn[8 * d8 + e];
+    }
+    auto unpack = [&](const u32x4_t& r, float (&xv)[8]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xv[2 * i] = __uint_as_float(r[i] << 16);
+        xv[2 * i + 1] = __uint_as_float(r[i] & 0xFFFF0000u);
+      }
+    };
+    for (int j0 = 0; j0 < nk; j0 += NG * kKB) {
+      const bool more = j0 + NG * kKB < nk;
+      float s[kKB];
+#pragma unroll
+      for (int uu = 0; uu < kKB; ++uu) {
+        const int jk = j0 + NG * uu + g;
+        float kx[8];
+        unpack(kr[uu], kx);
+        if (jk >= nk - 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) kx[e] = kme[e];
+        }
+        float pt = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pt = fmaf(q[e], kx[e], pt);
+        pt = sum8_dpp(pt);
+        s[uu] = jk < nk ? pt : -INFINITY;
+      }
+      if (more) kv_load(kr, Kc, j0 + NG * kKB);
+#pragma unroll
+      for (int c0 = 0; c0 < kKB; c0 += kSub) {
+        float bm = -INFINITY;
+#pragma unroll
+        for (int uu = c0; uu < c0 + kSub; ++uu) bm = fmaxf(bm, s[uu]);
+        if (bm == -INFINITY) continue;
+        const float mn = fmaxf(m_run, bm);
+        const float corr = __expf(m_run - mn);
+        l_run *= corr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o8[e] *= corr;
+#pragma unroll
+        for (int uu = c0; uu < c0 + kSub; ++uu) {
+          const int jk = j0 + NG * uu + g;
+          const float pr = __expf(s[uu] - mn);
+          l_run += pr;
+          float vx[8];
+          unpack(vr[uu], vx);
+          if (jk >= nk - 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) vx[e] = vme[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o8[e] = fmaf(pr, vx[e], o8[e]);
+        }
+        m_run = mn;
+      }
+      if (more) kv_load(vr, Vc, j0 + NG * kKB);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
+    if (d8 == 0) {
+      gm[g] = m_run;
+      gl[g] = l_run;
+    }
+  }
+  bar();
+  constexpr int NQ = 4, GPQ = 8;
+  float* qsum = pv + 32 * kPvPitch;
+  float* lsum = qsum + NQ * kPvPitch;
+  if (compute && act_u) {
+    const int dd = tu & (kHD - 1), qd = tu / kHD;
+    float M = -INFINITY;
+#pragma unroll 8
+    for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
+    float Ls = 0.f, a = 0.f;
+#pragma unroll
+    for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
+      const float wgt = __expf(gm[i] - M);
+      Ls = fmaf(gl[i], wgt, Ls);
+      a = fmaf(pv[i * kPvPitch + dd], wgt, a);
+    }
+    qsum[qd * kPvPitch + dd] = a;
+    if (dd == 0) lsum[qd] = Ls;
+  }
+  bar();
+  uint16_t* obf = reinterpret_cast<uint16_t*>(smem + L_OBF);
+  if (compute && tu < kHD) {
+    float v = 0.f;
+    if (act_u) {
+      float Ls = 0.f, a = 0.f;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        Ls += lsum[i];
+        a += qsum[i * kPvPitch + tu];
+      }
+      v = a / Ls;
+    }
+    obf[u * kHD + tu] = f2bf(v);
+  }
+  bar();
+  if (compute && (tu & 0xff) < 8) {  // o rows -> the cluster's [32][128] tile, write-through 16-B stores
+    const int d0 = 8 * (tu & 7);
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
+    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, ((c * 32 + r_u) * 128 + hh * kHD + d0) * 2, 0, 16);
+  }
+  drain();  // the o stores, and this wave's weight DMA (read from LDS from phase C on)
+  bar();
+  if (tid == 0) add_relaxed(cnt + CNT2 + c);
+
+  // ---- (C) attn.c_proj split c, tile j: decode_gemm_kernel EPI 2 arithmetic (one 16-deep k-step per wave)
+  if (tid == 0 && !poll_ge(cnt + CNT2 + c, kCPC * L1, err, 2)) *abort_flag = 1;
+  bar();
+  if (*abort_flag) return;
+  const int r32 = lane & 31, hb = lane >> 5;
+  if (compute) {
+    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x7fffffff, 0x00020000);
+    const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((c * 32 + r32) * 128 + 16 * w + 8 * hb) * 2, 0, 16);
+    const u32x4_t bb = *reinterpret_cast<const u32x4_t*>(smem + L_WO + w * 1024 + lane * 16);
+    f32x16_t acc32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
+    acc32 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t*>(&a),
+                                                    *reinterpret_cast<const bf16x8_t*>(&bb), acc32, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
+  }
+  bar();
+  auto store_partial = [&](float* dst) {  // 1024 outputs, 2 per thread; fixed-order sum over the waves
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int o = tid + 512 * k;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kNW; ++ww) v += red[ww * 1024 + o];
+      const int r = o >> 6, l = o & 63;
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      st_sc1_u32(reinterpret_cast<uint32_t*>(dst + ((int64_t)c * 32 + row) * kD + 32 * j + (l & 31)), __float_as_uint(v));
+    }
+  };
+  if (compute) {
+    store_partial(p1);
+    drain();
+  }
+  bar();
+  if (tid == 0) add_relaxed(cnt + CNT3 + j);
+
+  // ---- (D) x1 = x + (b_o + sum_c partial_c) on tile j (residual_reduce_ln_v4 order), x1^ -> cluster copy
+  if (tid == 0 && !poll_ge(cnt + CNT3 + j, kNC * L1, err, 3)) *abort_flag = 1;
+  bar();
+  if (*abort_flag) return;
+  float2 x1 = {0.f, 0.f};
+  if (compute) {
+    float2 pp = *reinterpret_cast<const float2*>(p.o_b + xcol);
+#pragma unroll
+    for (int cc = 0; cc < kNC; ++cc) {
+      const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p1 + ((int64_t)cc * 32 + xrow) * kD + xcol));
+      pp.x += __uint_as_float((uint32_t)v);
+      pp.y += __uint_as_float((uint32_t)(v >> 32));
+    }
+    x1 = float2{x_old.x + pp.x, x_old.y + pp.y};
+    st_sc1_u32(reinterpret_cast<uint32_t*>(xc + (((int64_t)c * 32 + xrow) * kD + xcol) * 2), pack2bf(x1.x, x1.y));
+    drain();
+  }
+  bar();
+  if (tid == 0) add_relaxed(cnt + CNT4 + c);
+
+  // ---- (E) c_fc (ln_2 folded) + gelu on tile 32c + j, A = the cluster's x1^ (decode_gemm16x FOLD)
+  if (tid == 0 && !poll_ge(cnt + CNT4 + c, kCPC * L1, err, 4)) *abort_flag = 1;
+  bar();
+  if (*abort_flag) return;
+  if (compute) {
+    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(xc, 0, 0x7fffffff, 0x00020000);
+    u32x4_t ax[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        ax[i][t] = __builtin_amdgcn_raw_buffer_load_b128(
+            rsrc, ((c * 32 + 16 * t + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, 16);
+    f32x4_t af[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+    float fs[2] = {0.f, 0.f}, fq[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(smem + L_WFC + (w + 8 * i) * 1024 + lane * 16);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&ax[i][t]);
+        af[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, af[t], 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = (float)a[e];
+          fs[t] += v;
+          fq[t] = fmaf(v, v, fq[t]);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float a = fs[t], s2 = fq[t];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (q4 == 0) {
+        rsum[w * 32 + 16 * t + c16] = a;
+        rsq[w * 32 + 16 * t + c16] = s2;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(w * 8 + 4 * t + r) * 64 + lane] = af[t][r];
+    }
+  }
+  bar();
+  if (tid < 32) {
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kNW; ++ww) {
+      S += rsum[ww * 32 + tid];
+      Q += rsq[ww * 32 + tid];
+    }
+    const float inv = 1.0f / kD, m = S * inv;
+    mu[tid] = m;
+    rsd[tid] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
+  }
+  bar();
+  uint16_t* ftile = obf;  // [32][16] bf16 (the o staging is consumed)
+  if (compute) {
+    const int e = tid >> 6, l = lane;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
+    const int row = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
+    const int n = (32 * c + j) * 16 + (l & 15);
+    v = rsd[row] * (v - mu[row] * p.fc_u[n]);
+    v += p.fc_c[n];
+    v = gelu_tanh_pl(v);
+    ftile[row * 16 + (l & 15)] = f2bf(v);
+  }
+  bar();
+  if (tid < 64) {  // [32 rows][16 columns] bf16 -> the cluster's f tile, write-through 16-B stores
+    const int row = tid >> 1, half = tid & 1;
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(ftile + row * 16 + 8 * half);
+    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(fcb, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, ((c * 32 + row) * 512 + 16 * j + 8 * half) * 2, 0, 16);
+    drain();
+  }
+  bar();
+  if (tid == 0) add_relaxed(cnt + CNT5 + c);
+
+  // ---- (F) mlp.c_proj split c, tile j: decode_gemm_kernel EPI 2 (k-steps w + 8i of the split)
+  if (tid == 0 && !poll_ge(cnt + CNT5 + c, kCPC * L1, err, 5)) *abort_flag = 1;
+  bar();
+  if (*abort_flag) return;
+  if (compute) {
+    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(fcb, 0, 0x7fffffff, 0x00020000);
+    u32x4_t a4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a4[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((c * 32 + r32) * 512 + 16 * (w + 8 * i) + 8 * hb) * 2, 0, 16);
+    f32x16_t acc32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc32 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+          *reinterpret_cast<const bf16x8_t*>(&a4[i]),
+          *reinterpret_cast<const bf16x8_t*>(smem + L_WPJ + (w + 8 * i) * 1024 + lane * 16), acc32, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
+  }
+  bar();
+  if (compute) {
+    store_partial(p2);
+    drain();
+  }
+  bar();
+  if (tid == 0) add_relaxed(cnt + CNT6 + j);
+
+  // ---- (G) x2 = x1 + (b_proj + sum_c partial_c); x, x^ for the next launch (cluster c: rows 4c .. 4c+3)
+  // The last layer stores x1 and leaves this reduce (with ln_f + final_norm, Q5) to itts_residual_reduce_ln.
+  if (p.last) {
+    if (compute && (xrow >> 2) == c && xrow < R)
+      *reinterpret_cast<float2*>(p.x + (int64_t)xrow * kD + xcol) = x1;
+    return;
+  }
+  if (tid == 0 && !poll_ge(cnt + CNT6 + j, kNC * L1, err, 6)) *abort_flag = 1;
+  bar();
+  if (*abort_flag) return;
+  if (compute && (xrow >> 2) == c && xrow < R) {
+    float2 pp = *reinterpret_cast<const float2*>(p.proj_b + xcol);
+#pragma unroll
+    for (int cc = 0; cc < kNC; ++cc) {
+      const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p2 + ((int64_t)cc * 32 + xrow) * kD + xcol));
+      pp.x += __uint_as_float((uint32_t)v);
+      pp.y += __uint_as_float((uint32_t)(v >> 32));
+    }
+    const float2 x2 = float2{x1.x + pp.x, x1.y + pp.y};
+    *reinterpret_cast<float2*>(p.x + (int64_t)xrow * kD + xcol) = x2;
+    *reinterpret_cast<uint32_t*>(p.xh + (int64_t)xrow * kD + xcol) = pack2bf(x2.x, x2.y);
+  }
+}
+
+int g_cu_count = -1;
+
+}  // namespace
+
+extern "C" int64_t itts_gpt_pl_scratch_bytes(void) { return kScratchBytes; }
+
+extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
+  if (!w || w->d_model != kD || w->n_head != kH || rows < 1 || rows > 32) return 0;
+  if (g_cu_count < 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 0;
+    g_cu_count = n;
+  }
+  return g_cu_count >= kWG ? 1 : 0;  // every workgroup must be resident at once (one per CU)
+}
+
+extern "C" int itts_gpt_pl_error(const void* scratch, void* stream, int* code) {
+  const char* fn = "itts_gpt_pl_error";
+  ITTS_REQUIRE(scratch && code, fn, "null pointer");
+  hipStream_t s = itts::as_stream(stream);
+  uint32_t v = 0;
+  if (hipMemcpyAsync(&v, static_cast<const unsigned char*>(scratch) + kOffErr, 4, hipMemcpyDeviceToHost,
+                     s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return itts::check_launch(fn);
+  *code = (int)v;
+  return 0;
+}
+
+extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl, const ItTsGptDecodeState* st,
+                                 int layer, int kstep, int last, void* scratch, void* stream) {
+  const char* fn = "itts_gpt_layer_pl";
+  ITTS_REQUIRE(ly && pl && st && scratch, fn, "null pointer");
+  ITTS_REQUIRE(pl->qkv_w12 && pl->qkv_uc && ly->o_w && ly->fc_w16 && ly->fc_u && ly->fc_c && ly->proj_w &&
+                   ly->proj_b && ly->o_c,
+               fn, "incomplete layer weights");
+  ITTS_REQUIRE(st->rows >= 1 && st->rows <= 32 && !st->kv_rows, fn, "1..32 rows, no beam lineage");
+  ITTS_REQUIRE(st->x && st->xh && st->k_cache && st->v_cache && st->tstate, fn, "null state buffer");
+  ITTS_REQUIRE((reinterpret_cast<uintptr_t>(scratch) & 255) == 0, fn, "scratch must be 256-B aligned");
+  const int64_t cache_hs = (int64_t)st->max_kv * kHD, cache_bs = (int64_t)kH * cache_hs;
+  const int64_t layer_cache = (int64_t)st->rows * cache_bs;
+  PlArgs a;
+  a.qkv_w12 = static_cast<const u32x4_t*>(pl->qkv_w12);
+  a.qkv_uc = pl->qkv_uc;
+  a.o_w = static_cast<const u32x4_t*>(ly->o_w);
+  a.o_b = ly->o_c;
+  a.fc_w16 = static_cast<const u32x4_t*>(ly->fc_w16);
+  a.fc_u = ly->fc_u;
+  a.fc_c = ly->fc_c;
+  a.proj_w = static_cast<const u32x4_t*>(ly->proj_w);
+  a.proj_b = ly->proj_b;
+  a.x = st->x;
+  a.xh = static_cast<uint16_t*>(st->xh);
+  a.kc = static_cast<uint16_t*>(st->k_cache) + layer * layer_cache;
+  a.vc = static_cast<uint16_t*>(st->v_cache) + layer * layer_cache;
+  a.cache_bs = cache_bs;
+  a.cache_hs = cache_hs;
+  a.pad = st->pad;
+  a.tstate = st->tstate;
+  a.kv_base = st->kv_base;
+  a.kstep = kstep;
+  a.R = st->rows;
+  a.layer = layer;
+  a.last = last;
+  a.eps = 1e-5f;
+  a.scratch = static_cast<unsigned char*>(scratch);
+  static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(gpt_layer_pl_kernel),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) == hipSuccess;
+  ITTS_REQUIRE(lds_ok, fn, "cannot reserve the kernel's LDS");
+  hipLaunchKernelGGL(gpt_layer_pl_kernel, dim3(kWG), dim3(kThreads), kLdsBytes, itts::as_stream(stream), a);
+  return itts::check_launch(fn);
+}
+
+// zero the step's counters and granules (one memset node ahead of the layer launches)
+extern "C" int itts_gpt_pl_begin_step(void* scratch, void* stream) {
+  const char* fn = "itts_gpt_pl_begin_step";
+  ITTS_REQUIRE(scratch, fn, "null pointer");
+  if (hipMemsetAsync(scratch, 0, kZeroBytes, itts::as_stream(stream)) != hipSuccess) return itts::check_launch(fn);
+  return 0;
+}
+
+extern "C" int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPlLayerW* pl, void* scratch,
+                                        const ItTsGptDecodeState* st, const ItTsSampling* smp, int nsteps,
+                                        void* stream) {
+  const char* fn = "itts_gpt_decode_steps_pl";
+  ITTS_REQUIRE(w && pl && scratch && st && smp && w->layers, fn, "null pointer");
+  ITTS_REQUIRE(nsteps >= 1 && nsteps <= 64, fn, "nsteps must be in [1, 64]");
+  ITTS_REQUIRE(smp->mode == 0 || smp->mode == 1, fn, "greedy / sampling only (beams: itts_gpt_decode_step)");
+  ITTS_REQUIRE(itts_gpt_pl_supported(w, st->rows), fn, "shape or device not supported (see itts_gpt_pl_supported)");
+  ITTS_REQUIRE(st->seen && st->done && st->codes && st->logits && w->head_w, fn, "sampler state missing");
+  const int L = w->n_layer, D = w->d_model, R = st->rows;
+  int rc = 0;
+  for (int k = 0; k < nsteps && rc == 0; ++k) {
+    rc = itts_gpt_pl_begin_step(scratch, stream);
+    for (int l = 0; l < L && rc == 0; ++l)
+      rc = itts_gpt_layer_pl(&w->layers[l], &pl[l], st, l, k, l + 1 == L, scratch, stream);
+    // the last layer's mlp.c_proj reduce with ln_f + final_norm (Q5) over the persistent partials
+    if (rc == 0)
+      rc = itts_residual_reduce_ln(st->x, D, reinterpret_cast<float*>(static_cast<unsigned char*>(scratch) + kOffP2),
+                                   kNC, (int64_t)32 * kD, kD, w->layers[L - 1].proj_b, st->xh, D, R, D, w->ln_f_g,
+                                   w->ln_f_b, w->final_g, w->final_b, ITTS_BF16, stream);
+    if (rc == 0) rc = itts::gpt_head_sample(w, st, smp, k, stream);
+  }
+  if (rc == 0) rc = itts_step_advance(st->tstate, nsteps, stream);
+  return rc;
+}

@@ -52,6 +52,7 @@ int decode_step_impl(const ItTsGptWeights* w, const ItTsGptDecodeState* st, cons
   ITTS_REQUIRE(st->x && st->xh && st->qkv && st->o && st->f && st->part && st->logits && st->k_cache && st->v_cache &&
                    st->tstate,
                fn, "null state buffer");
+  ITTS_REQUIRE(w->layers[0].o_w, fn, "ItTsGptLayerW.o_w (attn.c_proj, 32-column fragments) missing");
   ITTS_REQUIRE(smp->mode == 2 || (st->seen && st->done && st->codes), fn, "sampler state missing");
   const float eps = 1e-5f;
   const int64_t cache_hs = (int64_t)st->max_kv * kHD, cache_bs = (int64_t)H * cache_hs;
@@ -73,10 +74,15 @@ int decode_step_impl(const ItTsGptWeights* w, const ItTsGptDecodeState* st, cons
     else if (rc == 0)
       rc = itts_attn_decode(st->qkv, 3 * D, 1, (int64_t)R * 3 * D, nullptr, kc, vc, cache_bs, cache_hs, st->max_kv,
                             st->pad, st->kv_base + k, st->tstate, st->o, D, R, H, ITTS_BF16, ITTS_BF16, stream);
-    // attn.c_proj: x += o W_o + b_o, x^ = bf16(x)
+    // attn.c_proj: split-K 8 partials (one per head pair), then x += b_o + sum, x^ = bf16(x) -- the
+    // persistent layer's arithmetic (gpt_layer.hip: each cluster of 32 CUs owns two heads), so both
+    // paths give the same bits (round 3: one 16-column residual-epilogue launch, 5.4 us)
     if (rc == 0)
-      rc = itts_decode_gemm16x(st->o, D, ly.o_w16, D, D, R, ly.o_c, nullptr, eps, 0, 1, st->x, D, ITTS_F32, st->xh, D,
-                               8, stream);
+      rc = itts_decode_gemm(st->o, D, ly.o_w, D, D, R, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 2, st->part,
+                            D, ITTS_F32, (int64_t)R * D, kMlpSplit, stream);
+    if (rc == 0)
+      rc = itts_residual_reduce_ln(st->x, D, st->part, kMlpSplit, (int64_t)R * D, D, ly.o_c, st->xh, D, R, D, nullptr,
+                                   nullptr, nullptr, nullptr, ITTS_BF16, stream);
     // ln_2 (folded) + c_fc + gelu -> f bf16
     if (rc == 0)
       rc = itts_decode_gemm16x(st->xh, D, ly.fc_w16, D, 4 * D, R, ly.fc_c, ly.fc_u, eps, 1, 0, st->f, 4 * D, ITTS_BF16,
@@ -91,8 +97,17 @@ int decode_step_impl(const ItTsGptWeights* w, const ItTsGptDecodeState* st, cons
                                    last ? w->final_b : nullptr, ITTS_BF16, stream);
   }
   if (rc) return rc;
-  rc = itts_decode_gemm(st->xh, D, w->head_w, D, w->n_mel_codes, R, w->head_b, nullptr, nullptr, nullptr, nullptr, 0, 0,
-                        0, st->logits, w->logits_pitch, ITTS_F32, (int64_t)R * w->n_mel_codes, 1, stream);
+  return itts::gpt_head_sample(w, st, smp, k, stream);
+}
+}  // namespace
+
+// mel_head over x^ = final_norm(ln_f(x)) and the step's token selection + next embedding (shared by
+// the launch chain and the persistent layers)
+int itts::gpt_head_sample(const ItTsGptWeights* w, const ItTsGptDecodeState* st, const ItTsSampling* smp, int k,
+                          void* stream) {
+  const int D = w->d_model, R = st->rows;
+  int rc = itts_decode_gemm(st->xh, D, w->head_w, D, w->n_mel_codes, R, w->head_b, nullptr, nullptr, nullptr, nullptr,
+                            0, 0, 0, st->logits, w->logits_pitch, ITTS_F32, (int64_t)R * w->n_mel_codes, 1, stream);
   if (rc) return rc;
   if (smp->mode == 0) {
     rc = itts_sample_embed(st->logits, w->logits_pitch, w->n_mel_codes, st->seen, st->done, st->codes, st->max_new,
@@ -106,7 +121,6 @@ int decode_step_impl(const ItTsGptWeights* w, const ItTsGptDecodeState* st, cons
   }
   return rc;
 }
-}  // namespace
 
 extern "C" int itts_gpt_decode_step(const ItTsGptWeights* w, const ItTsGptDecodeState* st, const ItTsSampling* smp,
                                     void* stream) {

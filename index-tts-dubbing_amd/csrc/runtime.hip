@@ -25,7 +25,7 @@ int check_launch(const char* fn) {
 
 extern "C" const char* itts_last_error(void) { return itts::g_last_error.c_str(); }
 
-extern "C" int itts_abi_version(void) { return 2; }  // 2: sequence passes, multi-step decode
+extern "C" int itts_abi_version(void) { return 3; }  // 3: persistent decode layer, attn.c_proj split-K
 
 // Which gfx target this code object was built for (sanity check from the host).
 extern "C" const char* itts_build_target(void) { return "gfx950"; }
@@ -45,6 +45,7 @@ extern "C" int64_t itts_struct_size(int which) {
     case 8: return sizeof(ItTsBigvganWeights);
     case 9: return sizeof(ItTsGptSeqLayerW);
     case 10: return sizeof(ItTsGptSeqWeights);
+    case 11: return sizeof(ItTsGptPlLayerW);
     default: return -1;
   }
 }

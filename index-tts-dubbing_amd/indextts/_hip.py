@@ -89,6 +89,12 @@ SIGNATURES = {
     "itts_gpt_decode_state_bytes": (_c_i, [_vp, _c_i, _c_i, _c_i, _vp]),
     "itts_gpt_decode_step": (_c_i, [_vp, _vp, _vp, _vp]),
     "itts_gpt_decode_steps": (_c_i, [_vp, _vp, _vp, _c_i, _vp]),
+    "itts_gpt_pl_scratch_bytes": (_c_i64, []),
+    "itts_gpt_pl_supported": (_c_i, [_vp, _c_i]),
+    "itts_gpt_pl_begin_step": (_c_i, [_vp, _vp]),
+    "itts_gpt_layer_pl": (_c_i, [_vp, _vp, _vp, _c_i, _c_i, _c_i, _vp, _vp]),
+    "itts_gpt_pl_error": (_c_i, [_vp, _vp, ctypes.POINTER(_c_i)]),
+    "itts_gpt_decode_steps_pl": (_c_i, [_vp, _vp, _vp, _vp, _vp, _c_i, _vp]),
     "itts_bigvgan_workspace_bytes": (_c_i64, [_vp, _c_i, _c_i]),
     "itts_bigvgan_forward": (_c_i, [_vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _vp, _vp]),
 }
@@ -99,7 +105,11 @@ GPT_STATE_NBUF = 14  # itts_gpt_decode_state_bytes() entries
 # ---- structs of the whole-step entry point (include/itts_hip.h; field order is the ABI) ----------
 class GptLayerW(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("qkv_w16", "qkv_u", "qkv_c", "o_w16", "o_c", "fc_w16", "fc_u", "fc_c",
-                                   "proj_w", "proj_b")]
+                                   "proj_w", "proj_b", "o_w")]
+
+
+class GptPlLayerW(ctypes.Structure):
+    _fields_ = [("qkv_w12", _vp), ("qkv_uc", _vp)]
 
 
 class GptWeights(ctypes.Structure):

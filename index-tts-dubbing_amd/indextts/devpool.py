@@ -57,11 +57,14 @@ def _load_builder(spec: str):
 
 
 def _worker_main(conn, cfg_path: str, model_dir: str, is_fp16: bool, device: str,
-                 builder: str = "indextts.infer:IndexTTS"):
+                 builder: str = "indextts.infer:IndexTTS", no_pl: bool = False):
     """Child process: its own IndexTTS on ``device``; serves (rid, prompt, texts, max_tokens, gen).
     ``builder`` ("module:callable", the IndexTTS class by default) lets the CPU tests run the
-    protocol with a stand-in engine."""
+    protocol with a stand-in engine.  ``no_pl``: the device is shared with another engine, so the
+    persistent decode layer (which needs the whole GPU resident) is off (ITTS_PL=0)."""
     os.environ["ITTS_DEVICES"] = ""  # no nested pools
+    if no_pl:
+        os.environ["ITTS_PL"] = "0"
     try:
         tts = _load_builder(builder)(cfg_path=cfg_path, model_dir=model_dir, is_fp16=is_fp16, device=device)
         tts.LOOKAHEAD = 0
@@ -95,7 +98,7 @@ class DevicePool:
     workers load their weights while the parent builds its own engine)."""
 
     def __init__(self, cfg_path: str, model_dir: str, is_fp16: bool, devices: Sequence[str],
-                 builder: str = "indextts.infer:IndexTTS"):
+                 builder: str = "indextts.infer:IndexTTS", no_pl=()):
         ctx = mp.get_context("spawn")
         self.devices = list(devices)
         self.request_timeout = float(os.environ.get("ITTS_WORKER_TIMEOUT", "600"))
@@ -104,7 +107,8 @@ class DevicePool:
         self._rid = itertools.count()
         for d in self.devices:
             parent, child = ctx.Pipe(duplex=True)
-            p = ctx.Process(target=_worker_main, args=(child, cfg_path, model_dir, bool(is_fp16), d, builder),
+            p = ctx.Process(target=_worker_main, args=(child, cfg_path, model_dir, bool(is_fp16), d, builder,
+                                                       d in no_pl),
                             daemon=True, name=f"itts-worker-{d}")
             p.start()
             child.close()

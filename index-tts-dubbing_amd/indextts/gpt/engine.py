@@ -74,6 +74,29 @@ def fold_ln_weights(w_io, bias, ln, device):
             "N": wp.shape[0], "K": wp.shape[1]}
 
 
+def pack_qkv12(wx_qkv, w_io, ln, n_head: int = 16):
+    """Persistent-layer c_attn operands (gpt_layer.hip): workgroup b = 8j + c computes 12 columns of
+    head h = 2c + j/16 -- columns 12*(j%16) .. +11 of that head's [q | k | v] 192 -- from the SAME
+    rounded W' = diag(ln_1.g) W and fold terms u / c as itts_decode_gemm16x (``wx_qkv`` from
+    fold_ln_weights), in 16x16x32 B-fragment order without the 4 unused columns:
+    W12 [256][32 k-steps][4][12][8] bf16, uc [256][2][12] f32."""
+    w = _t(w_io).double()
+    g = _t(ln[0]).double()
+    wp = (w * g[:, None]).t().float().to(torch.bfloat16)  # W'^T [3D, D], as fold_ln_weights rounds it
+    N, K = wp.shape
+    D = N // 3
+    b = torch.arange(256)
+    cl, j = b % 8, b // 8
+    h = 2 * cl + j // 16
+    i = 12 * (j % 16)[:, None] + torch.arange(12)[None, :]          # [256, 12] index in the head's 192
+    cols = (i // 64) * D + h[:, None] * 64 + i % 64                   # c_attn output column
+    w12 = wp[cols.reshape(-1)].reshape(256, 12, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+    dev = wx_qkv["u"].device
+    cd = cols.to(dev)
+    uc = torch.stack([wx_qkv["u"][cd], wx_qkv["c"][cd]], 1).contiguous()  # the exact f32 fold terms
+    return {"w12": w12.to(dev), "uc": uc}
+
+
 class _Layer:
     pass
 
@@ -122,6 +145,10 @@ class HipGPT:
         #    reference); multi-role launches and a side-stream K/V prefetch were measured slower
         #    (profiles/ubench_fused_r02.txt)
         self.cstep = self.fold and os.environ.get("ITTS_CSTEP", "1") != "0"
+        #  * every layer of the step as ONE persistent launch (itts_gpt_decode_steps_pl, gpt_layer.hip) for
+        #    1..32 rows of the IndexTTS-1.5 shape on a 256-CU device; bit-identical to the launch chain
+        #    (ITTS_PL=0: the chain)
+        self.pl = self.cstep and os.environ.get("ITTS_PL", "1") != "0" and self.D == 1024 and self.H == 16
         self.layers: List[_Layer] = []
         for i in range(self.L):
             p = f"gpt.h.{i}"
@@ -141,6 +168,8 @@ class HipGPT:
                                                None if ln is None else (sd[f"{p}.ln_{1 if n == 'qkv' else 2}.weight"],
                                                                         sd[f"{p}.ln_{1 if n == 'qkv' else 2}.bias"]),
                                                dev)
+            if self.pl:
+                ly.pl = pack_qkv12(ly.wx["qkv"], sd[f"{p}.attn.c_attn.weight"], (sd[f"{p}.ln_1.weight"], None))
             if self.fuse_o:  # attn.c_proj in HF Conv1D [in, out] order (bf16) for the fused attention
                 ly.wo_io = sd[f"{p}.attn.c_proj.weight"].float().to(torch.bfloat16).contiguous().to(dev)
             self.layers.append(ly)
@@ -148,6 +177,12 @@ class HipGPT:
         self.head_b = f32("mel_head.bias")
         if self.fold:
             self._cweights = self._c_weights()
+        if self.pl:
+            self._plw = (_hip.GptPlLayerW * self.L)(*[_hip.GptPlLayerW(ly.pl["w12"].data_ptr(), ly.pl["uc"].data_ptr())
+                                                     for ly in self.layers])
+            n = int(self.lib.itts_gpt_pl_scratch_bytes())
+            self._pl_scratch = torch.zeros(n // 4 + 64, dtype=torch.float32, device=dev)  # 256-B aligned base
+            self._pl_err = self._pl_scratch[n // 4 - 64:]  # the sticky error word's block (re-armed per generate)
         self._lanes = {}  # lane index -> decode state, captured graph, stream
         self.step_events = None  # set to a list to time every decode step with HIP events (bench.py)
         self.logits_trace = None  # set to a list to record every step's raw logits [B, V] (tests)
@@ -410,7 +445,7 @@ class HipGPT:
             arr[i] = _hip.GptLayerW(wx["qkv"]["w16"].data_ptr(), wx["qkv"]["u"].data_ptr(), wx["qkv"]["c"].data_ptr(),
                                     wx["o"]["w16"].data_ptr(), wx["o"]["c"].data_ptr(), wx["fc"]["w16"].data_ptr(),
                                     wx["fc"]["u"].data_ptr(), wx["fc"]["c"].data_ptr(), ly.w["proj"]["sk"].data_ptr(),
-                                    ly.b["proj"].data_ptr())
+                                    ly.b["proj"].data_ptr(), ly.w["o"]["sk"].data_ptr())
         w = _hip.GptWeights(L, self.D, self.H, self.V, self.Vp, self.start_mel, self.stop_mel, arr,
                             self.ln_f[0].data_ptr(), self.ln_f[1].data_ptr(), self.final_norm[0].data_ptr(),
                             self.final_norm[1].data_ptr(), self.head_w["sk"].data_ptr(), self.head_b.data_ptr(),
@@ -443,6 +478,12 @@ class HipGPT:
             mode = _hip.Sampling(1, int(min_new), float(penalty), float(smp[0]), int(smp[1]), float(smp[2]))
         cst = self._c_state(st)
         stream = _hip.stream_ptr()
+        if not beams and self._pl_ok(st):  # every layer one persistent launch (bit-identical to the chain)
+            _hip.check(self.lib.itts_gpt_decode_steps_pl(ctypes.byref(self._cweights), self._plw,
+                                                         self._pl_scratch.data_ptr(), ctypes.byref(cst),
+                                                         ctypes.byref(mode), int(nsteps), stream),
+                       "itts_gpt_decode_steps_pl")
+            return
         if nsteps > 1:
             assert not beams
             _hip.check(self.lib.itts_gpt_decode_steps(ctypes.byref(self._cweights), ctypes.byref(cst),
@@ -453,6 +494,21 @@ class HipGPT:
         if beams:
             self._beam_step(st, 1)
             _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
+
+    def _pl_ok(self, st):
+        """persistent layers for this state: <= 32 rows, a 256-CU device, and no other lane of this engine
+        decoding concurrently (two persistent grids could each hold part of the CUs)"""
+        return (self.pl and st["B"] <= 32 and not st.get("multi_lane", False)
+                and bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), st["B"])))
+
+    def pl_error(self):
+        """hand-off timeout code recorded by the persistent layers (0 = none); syncs the stream."""
+        if not self.pl:
+            return 0
+        code = ctypes.c_int(0)
+        _hip.check(self.lib.itts_gpt_pl_error(self._pl_scratch.data_ptr(), _hip.stream_ptr(), ctypes.byref(code)),
+                   "itts_gpt_pl_error")
+        return int(code.value)
 
     def _decode_step_fold(self, st, min_new, penalty):
         """bf16 product decode step, five launches per layer: c_attn (ln_1 folded) -> attention ->
@@ -478,7 +534,9 @@ class HipGPT:
                     qkv.data_ptr(), 3 * D, 1, B * 3 * D, None, kc.data_ptr(), vc.data_ptr(), kc.stride(0),
                     kc.stride(1), self.max_kv, st["pad"].data_ptr(), st["s"] + 1, st["t"].data_ptr(), o.data_ptr(), D,
                     B, self.H, _hip.dtype_code(kc), _hip.dtype_code(o), stream), "itts_attn_decode")
-            self._dgx(o, ly.wx["o"], B, x, epi=1, xh=h)
+            # attn.c_proj: split-K 8 partials (head pairs) + reduce (gpt_step.hip / gpt_layer.hip arithmetic)
+            self._dg(o, ly.w["o"], B, None, st["ws"], epi=2, ksplit=8)
+            self._reduce(st, 8, ly.b["o"], (None, None))
             self._dgx(h, ly.wx["fc"], B, f, gelu=True)
             last = li + 1 == self.L
             if self.proj_fullk and not last:
@@ -668,11 +726,15 @@ class HipGPT:
         sampling = (float(temperature), int(top_k), float(top_p)) if do_sample else None
         if do_sample and seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None, self.cstep)
+        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None, self.cstep, self.pl)
         main = torch.cuda.current_stream(self.dev)
         work = []
-        for i, (r0, r1) in enumerate(self._lane_bounds(B, lanes)):
+        bounds = self._lane_bounds(B, lanes)
+        for i, (r0, r1) in enumerate(bounds):
             ln = self._lane(i, r1 - r0, max_new_tokens, s)
+            if ln["st"].get("multi_lane", False) != (len(bounds) > 1):
+                ln["st"]["multi_lane"] = len(bounds) > 1
+                ln["graph"] = ln["multi"] = None  # captured for the other decode path
             ln["stream"].wait_stream(main)  # inputs prepared on the caller's stream
             with torch.cuda.stream(ln["stream"]):
                 self._start_lane(ln, emb[r0:r1], pad[r0:r1], s, r0, sampling, seed,
@@ -723,6 +785,11 @@ class HipGPT:
                     break
         for ln in work:
             main.wait_stream(ln["stream"])
+            if self.pl and self._pl_ok(ln["st"]):
+                with torch.cuda.stream(ln["stream"]):
+                    code = self.pl_error()
+                if code:
+                    raise _hip.HipError(f"persistent decode layer: hand-off timeout (code {code})")
         codes = torch.cat([ln["st"]["codes"][:, :steps] for ln in work], 0).long()
         hit = codes == self.stop_mel
         if bool(hit.any(dim=1).all()):
@@ -735,6 +802,8 @@ class HipGPT:
         st = ln["st"]
         B = st["B"]
         st["s"] = s
+        if self.pl:
+            self._pl_err.zero_()
         st["pad"].copy_(pad)  # never rebind: the captured graph holds this pointer
         st["seen"].zero_()
         st["seen"][:, 1] = 1

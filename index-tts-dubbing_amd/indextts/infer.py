@@ -110,8 +110,14 @@ class IndexTTS:
             workers.remove(self.device)  # this process is the listed device's engine
         elif workers and self.device == "cuda" and "cuda:0" in workers:
             workers.remove("cuda:0")
+        # the persistent decode layer needs every one of its workgroups resident at once: on a GPU that
+        # several engines share (ITTS_DEVICES listing one device twice -- the tests' stand-in for two
+        # GPUs) their grids could each hold part of the CUs, so those engines use the launch chain
+        # (bit-identical results)
+        every = [self.device] + workers
+        shared = {d for d in every if every.count(d) > 1}
         if workers:
-            self._pool = DevicePool(cfg_path, model_dir, self.is_fp16, workers)
+            self._pool = DevicePool(cfg_path, model_dir, self.is_fp16, workers, no_pl=shared)
         # the fused anti-alias activation is always the HIP kernel here; kept for API compatibility
         self.use_cuda_kernel = use_cuda_kernel is None or bool(use_cuda_kernel)
         self.cfg = load_config(cfg_path)
@@ -127,6 +133,8 @@ class IndexTTS:
         print(">> bigvgan weights restored from:", self.bigvgan_path)
         self.engine = BatchedTTS(gpt_sd, bv_sd, self.cfg, self.device, dtype="bf16" if self.is_fp16 else "f32")
         self.gpt, self.bigvgan = self.engine.gpt, self.engine.vocoder
+        if self.device in shared:
+            self.gpt.pl = False
         del gpt_sd, bv_sd
 
         self.bpe_path = os.path.join(model_dir, self.cfg.dataset["bpe_model"])

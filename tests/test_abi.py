@@ -51,7 +51,7 @@ def test_ctypes_table_matches_header():
 
 
 def test_runtime_queries(lib):
-    assert lib.itts_abi_version() == 2
+    assert lib.itts_abi_version() == 3
     assert lib.itts_build_target() == b"gfx950"
 
 
@@ -84,7 +84,7 @@ def test_step_struct_layouts_match(lib):
     from indextts import _hip
     for i, c in enumerate((_hip.GptLayerW, _hip.GptWeights, _hip.GptDecodeState, _hip.Sampling, _hip.Conv, _hip.Act,
                            _hip.AmpLayer, _hip.BigvganStage, _hip.BigvganWeights, _hip.GptSeqLayerW,
-                           _hip.GptSeqWeights)):
+                           _hip.GptSeqWeights, _hip.GptPlLayerW)):
         assert lib.itts_struct_size(i) == ctypes.sizeof(c), c.__name__
     assert lib.itts_struct_size(99) == -1
     w = _hip.GptWeights(2, 256, 4, 8194, 8208, 8192, 8193)

@@ -75,10 +75,12 @@ def test_decode_step_through_the_abi_only():
         o = fold_ln_weights(sd[p + "attn.c_proj.weight"], sd[p + "attn.c_proj.bias"], None, dev)
         fc = fold_ln_weights(sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"], ln(i, 2), dev)
         proj = pack_skinny(_t(sd[p + "mlp.c_proj.weight"]).float().t().contiguous()).to(dev)
-        keep.extend([qkv, o, fc, proj])
+        ow = pack_skinny(_t(sd[p + "attn.c_proj.weight"]).float().t().contiguous()).to(dev)  # 32-column, split-K
+        keep.extend([qkv, o, fc, proj, ow])
         layers[i] = _hip.GptLayerW(qkv["w16"].data_ptr(), qkv["u"].data_ptr(), qkv["c"].data_ptr(),
                                    o["w16"].data_ptr(), o["c"].data_ptr(), fc["w16"].data_ptr(), fc["u"].data_ptr(),
-                                   fc["c"].data_ptr(), proj.data_ptr(), dev32(sd[p + "mlp.c_proj.bias"]))
+                                   fc["c"].data_ptr(), proj.data_ptr(), dev32(sd[p + "mlp.c_proj.bias"]),
+                                   ow.data_ptr())
     head = pack_skinny(_t(sd["mel_head.weight"]).float().contiguous()).to(dev)
     keep.append(head)
     w = _hip.GptWeights(L, D, H, V, Vp, start, stop, layers, dev32(sd["gpt.ln_f.weight"]),
@@ -185,10 +187,12 @@ def test_prefill_decode_latent_through_the_abi_only(size):
         o = fold_ln_weights(sd[p + "attn.c_proj.weight"], sd[p + "attn.c_proj.bias"], None, dev)
         fc = fold_ln_weights(sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"], lnp(i, 2), dev)
         proj = pack_skinny(_t(sd[p + "mlp.c_proj.weight"]).float().t().contiguous()).to(dev)
-        keep.extend([qkv, o, fc, proj])
+        ow = pack_skinny(_t(sd[p + "attn.c_proj.weight"]).float().t().contiguous()).to(dev)  # 32-column, split-K
+        keep.extend([qkv, o, fc, proj, ow])
         layers[i] = _hip.GptLayerW(qkv["w16"].data_ptr(), qkv["u"].data_ptr(), qkv["c"].data_ptr(),
                                    o["w16"].data_ptr(), o["c"].data_ptr(), fc["w16"].data_ptr(), fc["u"].data_ptr(),
-                                   fc["c"].data_ptr(), proj.data_ptr(), dev32(sd[p + "mlp.c_proj.bias"]))
+                                   fc["c"].data_ptr(), proj.data_ptr(), dev32(sd[p + "mlp.c_proj.bias"]),
+                                   ow.data_ptr())
         ig = []
         for k in ("attn.c_attn", "attn.c_proj", "mlp.c_fc", "mlp.c_proj"):
             wt = _t(sd[p + k + ".weight"]).float().t().contiguous()  # HF Conv1D [in, out] -> [out, in]
