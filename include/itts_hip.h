@@ -185,6 +185,12 @@ int itts_relu_affine_rows(const float* x, int64_t x_sb, int64_t ldx, int B, int 
  * an utterance's statistics do not depend on the batch. */
 int itts_time_stats(const float* x, int64_t x_sb, int64_t ldx, const float* logits, int64_t l_sb, int64_t ldl, int B,
                     int T, int C, float eps, float* mean, float* stdv, void* stream);
+/* PerceiverResampler cross-attention (gpt/perceiver.py:111-150 Attend, :296-317 Attention) of 32 latent
+ * queries q [B][32][ldq] over keys / values [B][nk][ldkv] (head h at columns 64h .. 64h+63, f32),
+ * key_mask [B][nk] u8 (0 = masked, NULL = none): out[b][i][64h + d] f32, row-independent. */
+int itts_cross_attn(const float* q, int64_t q_sb, int64_t ldq, const float* k, const float* v, int64_t kv_sb,
+                    int64_t ldkv, const uint8_t* key_mask, int B, int nq, int nk, int heads, float scale, float* out,
+                    int64_t o_sb, int64_t ldo, void* stream);
 /* itts_cond_rel_attn -- RelPositionMultiHeadedAttention (gpt/conformer/attention.py:235-312, no rel_shift),
  * head dim 64, H heads (C = 64 H): qkv f32 [B][T][ld_qkv] = (q | k | v) linear outputs, pos f32 [T][ld_pos]
  * = linear_pos(pos_emb), bias_u / bias_v [H][64]; score = ((q+u).k + (q+v).p) * scale over keys t < lens[b]

@@ -402,6 +402,63 @@ __global__ __launch_bounds__(1024) void time_stats_kernel(const float* __restric
   if (on && sl == 0) stdv[(int64_t)b * C + c] = sqrtf(fmaxf(v, eps));
 }
 
+
+// ---- perceiver cross-attention (PerceiverResampler Attention, gpt/perceiver.py:111-150, 296-317) ----
+// out[b][i][h*64 + d] = softmax_j(q_i . k_j * scale, keys with key_mask[b][j] == 0 excluded) . v_j, f32,
+// one workgroup per (head, prompt): 256 threads = the 32 latent queries x 8 lanes (8 dims each, DPP
+// sums), keys streamed through LDS in 64-key tiles with an online softmax in a fixed order -- a
+// prompt's result does not depend on the other prompts in the batch (the torch batched-GEMM form did,
+// by up to 5e-3 rel-RMS).  The reference fills masked scores with -finfo.max; the 32 latent keys are
+// never masked, so dropping masked keys is the same softmax.
+constexpr int kXq = 32, kXt = 64;
+__global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict__ q, int64_t q_sb, int64_t ldq,
+                                                         const float* __restrict__ k, const float* __restrict__ v,
+                                                         int64_t kv_sb, int64_t ldkv, const uint8_t* __restrict__ kmask,
+                                                         int nk, float scale, float* __restrict__ out, int64_t o_sb,
+                                                         int64_t ldo) {
+  __shared__ float Ks[kXt][65], Vs[kXt][65];
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, qi = tid >> 3, d8 = tid & 7;
+  float qv[8], o[8];
+  const float* qr = q + (int64_t)b * q_sb + (int64_t)qi * ldq + h * 64 + 8 * d8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    qv[e] = qr[e] * scale;
+    o[e] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  const float* kb = k + (int64_t)b * kv_sb + h * 64;
+  const float* vb = v + (int64_t)b * kv_sb + h * 64;
+  const uint8_t* mk = kmask ? kmask + (int64_t)b * nk : nullptr;
+  for (int j0 = 0; j0 < nk; j0 += kXt) {
+    __syncthreads();
+    for (int e = tid; e < kXt * 64; e += 256) {
+      const int r = e >> 6, d = e & 63, jj = j0 + r;
+      Ks[r][d] = jj < nk ? kb[(int64_t)jj * ldkv + d] : 0.f;
+      Vs[r][d] = jj < nk ? vb[(int64_t)jj * ldkv + d] : 0.f;
+    }
+    __syncthreads();
+    const int n = min(kXt, nk - j0);
+    for (int r = 0; r < n; ++r) {
+      if (mk && !mk[j0 + r]) continue;  // uniform over the workgroup
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s = fmaf(qv[e], Ks[r][8 * d8 + e], s);
+      s = sum8_dpp(s);
+      const float mn = fmaxf(m, s);
+      const float corr = __expf(m - mn), pr = __expf(s - mn);
+      l = l * corr + pr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(pr, Vs[r][8 * d8 + e], o[e] * corr);
+      m = mn;
+    }
+  }
+  float* orow = out + (int64_t)b * o_sb + (int64_t)qi * ldo + h * 64 + 8 * d8;
+  const float inv = 1.0f / l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) orow[e] = o[e] * inv;
+}
+
 }  // namespace
 
 extern "C" int itts_time_stats(const float* x, int64_t x_sb, int64_t ldx, const float* logits, int64_t l_sb,
@@ -504,5 +561,18 @@ extern "C" int itts_cond_glu_dwconv(const float* a, int64_t lda, int B, int T, i
   const int threads = ((C / 4 + 63) / 64) * 64;
   hipLaunchKernelGGL(glu_dwconv_kernel, dim3(T, B), dim3(threads), 0, itts::as_stream(stream), a, lda, T, C, w,
                      w_bias, K, ln_g, ln_b, eps, static_cast<uint16_t*>(y), ldy);
+  return itts::check_launch(fn);
+}
+
+extern "C" int itts_cross_attn(const float* q, int64_t q_sb, int64_t ldq, const float* k, const float* v, int64_t kv_sb,
+                               int64_t ldkv, const uint8_t* key_mask, int B, int nq, int nk, int heads, float scale,
+                               float* out, int64_t o_sb, int64_t ldo, void* stream) {
+  const char* fn = "itts_cross_attn";
+  ITTS_REQUIRE(B >= 0 && heads > 0 && nk >= 1, fn, "bad sizes");
+  if (B == 0) return 0;
+  ITTS_REQUIRE(q && k && v && out, fn, "null pointer");
+  ITTS_REQUIRE(nq == kXq, fn, "32 latent queries (PerceiverResampler num_latents)");
+  hipLaunchKernelGGL(cross_attn_kernel, dim3(heads, B), dim3(256), 0, itts::as_stream(stream), q, q_sb, ldq, k, v,
+                     kv_sb, ldkv, key_mask, nk, scale, out, o_sb, ldo);
   return itts::check_launch(fn);
 }

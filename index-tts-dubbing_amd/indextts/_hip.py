@@ -51,6 +51,8 @@ SIGNATURES = {
     "itts_time_stats": (_c_i, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_f, _vp, _vp, _vp]),
     "itts_cond_rel_attn": (_c_i, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i, _c_i, _c_i, _c_f, _vp, _c_i64, _c_i,
                                   _vp]),
+    "itts_cross_attn": (_c_i, [_vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _c_i, _c_i, _c_i, _c_i, _c_f, _vp,
+                               _c_i64, _c_i64, _vp]),
     "itts_cond_subsample": (_c_i, [_vp, _c_i64, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _c_i, _vp, _vp]),
     "itts_cond_glu_dwconv": (_c_i, [_vp, _c_i64, _c_i, _c_i, _c_i, _vp, _vp, _c_i, _vp, _vp, _c_f, _vp, _c_i64, _vp,
                                     _vp]),

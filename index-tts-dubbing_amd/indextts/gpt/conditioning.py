@@ -1,9 +1,11 @@
 """Speech-prompt conditioning: conformer encoder + perceiver resampler -> ``conds [B, 32, D]``.
 
-Runs once per prompt (cached by the caller, quirk Q6), so it is PyTorch-ROCm code on the device
-rather than a hand-written kernel target.  Its convolutions are explicit
-im2col GEMMs (``utils/convgemm.py``: deterministic without MIOpen's naive direct kernel, §8(f) item 2).
-Functional restatement over the reference state-dict, device agnostic.
+Runs once per prompt (cached by the caller, quirk Q6).  With a ``lin`` bank (bf16 product mode,
+``utils/hiplinear.py``) every linear / pointwise conv runs on the HIP MFMA implicit GEMM and the
+subsampling conv, rel-pos attention, GLU / depthwise / LayerNorm / SiLU run as HIP kernels
+(csrc/cond_ops.hip); without it (f32 verification mode) it is f32 torch with
+the convolutions as explicit im2col GEMMs (``utils/convgemm.py``: deterministic without MIOpen's naive
+direct kernel).  Functional restatement over the reference state-dict.
 
 Reference behaviour followed (file:line in the reference tree):
   * ``UnifiedVoice.get_conditioning`` conformer_perceiver branch  gpt/model.py:496-502
@@ -127,15 +129,18 @@ def perceiver_resample(sd, ctx, key_mask, heads: int, prefix="perceiver_encoder"
         context = torch.cat([lat, x], dim=1)
         q = _lin(lat, sd, a + ".to_q", bias=False, lin=lin)
         kv = _lin(context, sd, a + ".to_kv", bias=False, lin=lin)
-        k, v = kv.chunk(2, dim=-1)
         B, n, inner = q.shape
         dh = inner // heads
-        q = q.view(B, n, heads, dh).transpose(1, 2)
-        k = k.view(B, -1, heads, dh).transpose(1, 2)
-        v = v.view(B, -1, heads, dh).transpose(1, 2)
-        sim = (q @ k.transpose(-2, -1)) * (dh ** -0.5)
-        sim = sim.masked_fill(~key_mask[:, None, None, :], neg)
-        out = (sim.softmax(dim=-1) @ v).transpose(1, 2).reshape(B, n, inner)
+        if lin is not None:  # product mode: the HIP cross-attention kernel (row-independent, f32)
+            out = lin.cross_attn(q, kv, key_mask, heads, dh ** -0.5)
+        else:
+            k, v = kv.chunk(2, dim=-1)
+            q = q.view(B, n, heads, dh).transpose(1, 2)
+            k = k.view(B, -1, heads, dh).transpose(1, 2)
+            v = v.view(B, -1, heads, dh).transpose(1, 2)
+            sim = (q @ k.transpose(-2, -1)) * (dh ** -0.5)
+            sim = sim.masked_fill(~key_mask[:, None, None, :], neg)
+            out = (sim.softmax(dim=-1) @ v).transpose(1, 2).reshape(B, n, inner)
         lat = _lin(out, sd, a + ".to_out", bias=False, lin=lin) + lat
         f = f"{prefix}.layers.{i}.1"
         hx, gate = _lin(lat, sd, f + ".0", lin=lin).chunk(2, dim=-1)

@@ -49,9 +49,14 @@ def _load_state_dict(path: str, key: Optional[str] = None) -> Dict[str, torch.Te
     return sd
 
 
+def _is_cue(e) -> bool:
+    """an object shaped like srt_dubbing's cue (srt_parser.SRTEntry: index, start_time, end_time, text and the
+    ``duration`` property the strategies read): a ``str`` text and a numeric duration"""
+    return isinstance(getattr(e, "text", None), str) and isinstance(getattr(e, "duration", None), (int, float))
+
+
 def _is_cue_list(v) -> bool:
-    return isinstance(v, (list, tuple)) and len(v) > 1 and all(
-        isinstance(getattr(e, "text", None), str) for e in v[:8])
+    return isinstance(v, (list, tuple)) and len(v) > 1 and all(_is_cue(e) for e in v[:8])
 
 
 def _caller_cue_texts(text: str, max_depth: int = 8) -> Optional[List[str]]:
@@ -60,11 +65,12 @@ def _caller_cue_texts(text: str, max_depth: int = 8) -> Optional[List[str]]:
     srt_dubbing's strategies iterate ``for i, entry in enumerate(entries)`` and call
     ``tts_engine.synthesize(text=entry.text, ...)`` (srt_dubbing/src/strategies/basic_strategy.py:65-74,
     stretch / hq_stretch / adaptive likewise) -> ``IndexTTSEngine.synthesize`` -> ``infer``
-    (tts_engines/index_tts_engine.py:45-63).  In each calling frame (innermost first) any local list
-    or tuple of objects with a ``str`` ``text`` attribute that contains ``text`` is a candidate (the one
-    named ``entries`` first); the caller's position is an ``int`` local that indexes a cue with this
-    text (the loop counter, whatever its name), else the first cue with this text.  None when no frame
-    holds such a list: then ``infer`` synthesises this text alone, exactly as the reference does."""
+    (tts_engines/index_tts_engine.py:45-63).  Kept narrow: in each calling frame
+    (innermost first) a local list or tuple of SRT-cue-shaped objects (a ``str`` ``text`` and a numeric
+    ``duration``, as ``SRTEntry``) is a candidate (the one named ``entries`` first) only when the same
+    frame also holds an ``int`` local that indexes a cue with exactly this text -- the loop counter of
+    ``for i, entry in enumerate(entries)``, whatever its name.  None otherwise: then ``infer``
+    synthesises this text alone, exactly as the reference does."""
     f = sys._getframe(2)
     try:
         for _ in range(max_depth):
@@ -78,7 +84,8 @@ def _caller_cue_texts(text: str, max_depth: int = 8) -> Optional[List[str]]:
                     continue
                 pos = next((v for v in loc.values() if type(v) is int and 0 <= v < len(texts) and texts[v] == text),
                            None)
-                return texts[texts.index(text) if pos is None else pos:]
+                if pos is not None:
+                    return texts[pos:]
             f = f.f_back
         return None
     finally:
@@ -251,8 +258,11 @@ class IndexTTS:
         min_new_tokens = kw.pop("min_new_tokens", 0)
         seed = kw.pop("seed", None)
         kw.pop("num_return_sequences", None)
-        if kw:
-            warnings.warn(f"ignored generation kwargs: {sorted(kw)}", RuntimeWarning)
+        if kw:  # e.g. inference_speech's typical_sampling / typical_mass (gpt/model.py:655-708; off by default)
+            warnings.warn(f"ignored generation kwargs: {sorted(kw)} -- the HIP decode honours do_sample, top_p, "
+                          "top_k, temperature, length_penalty, num_beams, repetition_penalty, max_mel_tokens, "
+                          "min_new_tokens, seed (INTEGRATION.md §2); the reference would pass the rest to "
+                          "inference_speech / HF generate", RuntimeWarning)
         num_beams = int(num_beams or 1)
         if num_beams > 16:
             raise ValueError("HIP beam search supports num_beams <= 16")
@@ -456,9 +466,9 @@ class IndexTTS:
         ITTS_DEVICES, dealt over this process's GPU and the worker GPUs), and keep one result per
         occurrence for the ``infer`` calls that follow with the same prompt (a path), text and
         arguments.  Deterministic decoding (``do_sample=False``): each result equals what that
-        ``infer`` call would have computed (rows never interact; tests/test_gpu_lookahead.py,
-        tests/test_gpu_devpool.py); with sampling it is an independent draw from the same
-        distribution, as a fresh call would be.  Results of an earlier window for the same arguments
+        ``infer`` call would have computed (rows never interact; tests/test_gpu_lookahead.py, and
+        tests/test_gpu_longform.py::test_two_engines_one_gpu_equal_per_call: two processes on one GPU,
+        short rows); with sampling it is an independent draw from the same distribution, as a fresh call would be.  Results of an earlier window for the same arguments
         that the caller has moved past are dropped."""
         key = self._ahead_key(audio_prompt, max_text_tokens_per_sentence, generation_kwargs)
         if key is None:

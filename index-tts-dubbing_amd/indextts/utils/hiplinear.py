@@ -192,6 +192,21 @@ class HipLinearBank:
             out.data_ptr(), C, _hip.BF16, _hip.stream_ptr(self.dev)), "itts_cond_rel_attn")
         return self(out, name + ".linear_out", out=residual, residual=residual)
 
+    def cross_attn(self, q: torch.Tensor, kv: torch.Tensor, key_mask: torch.Tensor, heads: int, scale: float):
+        """PerceiverResampler attention (gpt/perceiver.py:111-150): q [B, 32, H*64] f32, kv [B, nk, 2*H*64]
+        (k | v halves, to_kv's chunk order), key_mask [B, nk] bool -> [B, 32, H*64] f32 (itts_cross_attn,
+        one workgroup per (head, prompt): a prompt's conds do not depend on the batch)."""
+        q, kv = q.float().contiguous(), kv.float().contiguous()
+        B, n, inner = q.shape
+        nk = kv.shape[1]
+        km = key_mask.to(torch.uint8).contiguous()
+        out = torch.empty(B, n, inner, dtype=torch.float32, device=self.dev)
+        _hip.check(self.lib.itts_cross_attn(
+            q.data_ptr(), n * inner, inner, kv.data_ptr(), kv.data_ptr() + 4 * inner, nk * 2 * inner, 2 * inner,
+            km.data_ptr(), B, n, nk, heads, float(scale), out.data_ptr(), n * inner, inner,
+            _hip.stream_ptr(self.dev)), "itts_cross_attn")
+        return out
+
     # ---------------- ECAPA channel-last (vocoder/ecapa.py speaker_embedding_cl) ----------------
     def pad_rows(self, x: torch.Tensor, pad: int, reflect: bool = True, x2: Optional[torch.Tensor] = None,
                  cp: Optional[int] = None) -> torch.Tensor:

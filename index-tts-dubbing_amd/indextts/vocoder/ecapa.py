@@ -1,8 +1,11 @@
 """ECAPA-TDNN speaker embedding applied to the prompt mel inside every vocoder call.
 
-Deterministic and per-prompt, so the host caches it (quirk Q6); PyTorch-ROCm code, not a
-hand-written kernel target; convolutions as im2col GEMMs
-(``utils/convgemm.py``, §8(f) item 2).
+Deterministic and per-prompt, so the host caches it (quirk Q6).  Two numeric modes: the bf16 product
+mode (``speaker_embedding_cl``) runs channel-last on the HIP kernels -- every conv on the MFMA implicit
+GEMM over reflect-padded bf16 rows (``itts_pad_rows_bf16``), ReLU + BatchNorm as one affine kernel,
+the pooling statistics in ``itts_time_stats`` (csrc/cond_ops.hip); the f32
+verification mode (``speaker_embedding``) is f32 torch with the convolutions as im2col GEMMs
+(``utils/convgemm.py``), the path the fp32 fixtures pin.
 
 Reference behaviour followed:
   * ``ECAPA_TDNN.forward``                       BigVGAN/ECAPA_TDNN.py:543-581 (lengths=None)

@@ -547,3 +547,43 @@ def test_time_stats_matches_torch(B, T, C, att):
     assert float(((gs.cpu() - std).abs() / (std.abs() + 1)).max()) <= 1e-5
     m1, s1 = bank.time_stats(x[-1:].cuda(), None if lg is None else lg[-1:].cuda())
     assert torch.equal(m1[0], gm[-1]) and torch.equal(s1[0], gs[-1])
+
+
+@pytest.mark.parametrize("nk,masked", [(287, False), (100, True), (33, False)])
+def test_cross_attn_matches_torch(nk, masked):
+    """itts_cross_attn (PerceiverResampler attention, gpt/perceiver.py:111-150) vs torch fp32 on the same
+    q / k / v: |err| <= 1e-5 relative to max|v|; masked keys excluded (the reference fills them with
+    -finfo.max; the 32 latent keys are never masked); each prompt bit-identical alone and in a batch."""
+    _hip, lib = _lib()
+    g = torch.Generator().manual_seed(nk)
+    B, H, n = 3, 8, 32
+    inner = 64 * H
+    q = torch.randn(B, n, inner, generator=g)
+    kv = torch.randn(B, nk, 2 * inner, generator=g)
+    km = torch.ones(B, nk, dtype=torch.bool)
+    if masked:
+        km[1, 60:] = False
+        km[2, 40:] = False
+    scale = 64 ** -0.5
+
+    def run(qq, kvv, kmm):
+        Bq = qq.shape[0]
+        out = torch.empty(Bq, n, inner, device="cuda")
+        qd, kd, md = qq.contiguous().cuda(), kvv.contiguous().cuda(), kmm.to(torch.uint8).contiguous().cuda()
+        _hip.check(lib.itts_cross_attn(qd.data_ptr(), n * inner, inner, kd.data_ptr(), kd.data_ptr() + 4 * inner,
+                                       nk * 2 * inner, 2 * inner, md.data_ptr(), Bq, n, nk, H, scale, out.data_ptr(),
+                                       n * inner, inner, _hip.stream_ptr()), "cross_attn")
+        torch.cuda.synchronize()
+        return out.cpu()
+
+    got = run(q, kv, km)
+    k, v = kv.chunk(2, -1)
+    qh = q.view(B, n, H, 64).transpose(1, 2)
+    kh = k.reshape(B, nk, H, 64).transpose(1, 2)
+    vh = v.reshape(B, nk, H, 64).transpose(1, 2)
+    sim = (qh @ kh.transpose(-2, -1)) * scale
+    sim = sim.masked_fill(~km[:, None, None, :], -torch.finfo(sim.dtype).max)
+    ref = (sim.softmax(-1) @ vh).transpose(1, 2).reshape(B, n, inner)
+    assert float((got - ref).abs().max()) <= 1e-5 * float(v.abs().max())
+    one = run(q[1:2], kv[1:2], km[1:2])
+    assert torch.equal(one[0], got[1])
