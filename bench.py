@@ -323,10 +323,15 @@ def main():
         d_bytes = sum(tts.gpt.step_weight_bytes + keys * tts.gpt.kv_bytes_per_key for _, _, _, keys in step_ev)
         gbs = d_bytes / (d_ms * 1e-3) / 1e9
         rows = step_ev[0][2]
-        dec = {"kernel": f"GPT decode step, {rows} rows (hipGraph: 20 x [c_attn GEMM (ln_1 folded), attention, "
-                         "attn.c_proj GEMM (residual epilogue), c_fc GEMM (ln_2 folded, gelu), mlp.c_proj GEMM "
-                         "(split-K 8), reduce] + mel_head GEMM + " + ("beam candidates/select)" if args.decoding == "beam3"
-                                                                       else "sampler)"), "bound": "hbm",
+        pl = tts.gpt.pl and rows <= 32 and args.decoding != "beam3"
+        body = ("20 x ONE persistent launch per layer (gpt_layer.hip: c_attn (ln_1 folded) -> attention -> "
+                "attn.c_proj split-K 8 + reduce -> c_fc (ln_2 folded, gelu) -> mlp.c_proj split-K 8 + reduce as "
+                "phases joined by in-launch hand-offs, weights prefetched by LDS-DMA) + counter memset + "
+                "last-layer reduce/ln_f/final_norm" if pl else
+                "20 x [c_attn GEMM (ln_1 folded), attention, attn.c_proj GEMM split-K 8, reduce, c_fc GEMM "
+                "(ln_2 folded, gelu), mlp.c_proj GEMM (split-K 8), reduce]")
+        dec = {"kernel": f"GPT decode step, {rows} rows (hipGraph: {body} + mel_head GEMM + " +
+                         ("beam candidates/select)" if args.decoding == "beam3" else "sampler)"), "bound": "hbm",
                "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
                "traffic": None, "launches": len(step_ev), "avg_launch_us": round(1e3 * d_ms / len(step_ev), 2),
                "algorithmic_bytes_per_launch": round(d_bytes / len(step_ev)), "share_of_step": round(d_ms / (1e3 * dt), 3)}

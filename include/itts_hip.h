@@ -453,9 +453,9 @@ int itts_gpt_decode_steps(const ItTsGptWeights* w, const ItTsGptDecodeState* sta
 /* ---- persistent decode layer (gpt_layer.hip) ----------------------------------------------------
  * One GPT-2 block of the decode step (HF modeling_gpt2.py:246-306 via gpt/model.py:115-192) as ONE
  * launch of 256 workgroups (one per CU) joined by in-launch hand-offs, each workgroup's weights
- * requested at the start of the launch.  IndexTTS-1.5 shapes (d_model 1024, 16 heads) and 1..32 rows,
- * no beam lineage; bit-identical to the launch chain (itts_gpt_decode_steps).  Extra weights per layer
- * besides ItTsGptLayerW: */
+ * requested at the start of the launch.  IndexTTS-1.5 shapes (d_model 1024, 16 heads), 1..128 rows,
+ * with or without the beam lineage table (state.kv_rows); bit-identical to the launch chain
+ * (itts_gpt_decode_step[s]).  Extra weights per layer besides ItTsGptLayerW: */
 typedef struct ItTsGptPlLayerW {
   const void* qkv_w12;  /* c_attn (ln_1 folded), 12 columns per workgroup: [256][32][4][12][8] bf16 */
   const float* qkv_uc;  /* [256][2][12]: u and c of those columns (itts_decode_gemm16x fold terms) */
@@ -465,8 +465,8 @@ typedef struct ItTsGptPlLayerW {
 int64_t itts_gpt_pl_scratch_bytes(void);
 /* 1 if the persistent path runs this shape on the current device (256 CUs resident at once), else 0. */
 int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows);
-/* Zero the step's hand-off counters (a memset node); once before the layers of every decode step. */
-int itts_gpt_pl_begin_step(void* scratch, void* stream);
+/* Zero the step's hand-off counters and granules (a memset node); once before the layers of every step. */
+int itts_gpt_pl_begin_step(void* scratch, int rows, void* stream);
 /* Layer `layer` of decode step `kstep` of a multi-step call (key kv_base + t + kstep); `last`: leave
  * the mlp.c_proj reduce (+ ln_f + final_norm) to itts_residual_reduce_ln over the scratch partials. */
 int itts_gpt_layer_pl(const ItTsGptLayerW* layer_w, const ItTsGptPlLayerW* pl, const ItTsGptDecodeState* state,
@@ -474,7 +474,8 @@ int itts_gpt_layer_pl(const ItTsGptLayerW* layer_w, const ItTsGptPlLayerW* pl, c
 /* A hand-off timeout recorded in the scratch (0 = none; else every later layer launch returns at once
  * and the results are invalid until the scratch is zeroed again).  Synchronises `stream`. */
 int itts_gpt_pl_error(const void* scratch, void* stream, int* code);
-/* itts_gpt_decode_steps with every layer on the persistent path (pl: [n_layer]). */
+/* itts_gpt_decode_steps with every layer on the persistent path (pl: [n_layer]); sampling mode 2 (beams:
+ * logits only, nsteps = 1, the caller runs the beam kernels and the step advance) as itts_gpt_decode_step. */
 int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPlLayerW* pl, void* scratch,
                              const ItTsGptDecodeState* state, const ItTsSampling* sampling, int nsteps, void* stream);
 

@@ -51,17 +51,19 @@ constexpr int kKB = 8;                                // attention keys per grou
 constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
 constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s), then the grid drains
 
-// scratch layout (bytes); the first kZeroBytes are zeroed before every step
-constexpr int64_t kOffCnt = 0, kCntWords = 128;
-constexpr int64_t kOffGq = 512;                                    // [16 heads][32 rows][192] u64
-constexpr int64_t kOffOb = kOffGq + (int64_t)kH * 32 * 192 * 8;    // [8][32][128] bf16
-constexpr int64_t kOffP1 = kOffOb + (int64_t)kNC * 32 * 128 * 2;   // [8][32][1024] f32
-constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * 32 * kD * 4;    // [8][32][1024] bf16
-constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * 32 * kD * 2;    // [8][32][512] bf16
-constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * 32 * 512 * 2;   // [8][32][1024] f32
-constexpr int64_t kOffErr = kOffP2 + (int64_t)kNC * 32 * kD * 4;  // sticky error word (not zeroed per step)
+// scratch layout (bytes) for up to kMaxR rows; the counters and the granules of the step's rows are zeroed
+// before every step
+constexpr int kMaxR = 128;
+constexpr int64_t kOffCnt = 0;
+constexpr int64_t kOffGq = 512;                                       // [128 rows][16 heads][192] u64
+constexpr int64_t kOffOb = kOffGq + (int64_t)kMaxR * kH * 192 * 8;    // [8][128][128] bf16
+constexpr int64_t kOffP1 = kOffOb + (int64_t)kNC * kMaxR * 128 * 2;   // [8][128][1024] f32
+constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * kMaxR * kD * 4;    // [8][128][1024] bf16
+constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * kMaxR * kD * 2;    // [8][128][512] bf16
+constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * kMaxR * 512 * 2;   // [8][128][1024] f32
+constexpr int64_t kOffErr = kOffP2 + (int64_t)kNC * kMaxR * kD * 4;   // sticky error word (not zeroed per step)
 constexpr int64_t kScratchBytes = kOffErr + 256;
-constexpr int64_t kZeroBytes = kOffOb;  // counters + granules
+inline int64_t zero_bytes(int rows) { return kOffGq + (int64_t)rows * kH * 192 * 8; }  // multiple of 16
 enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56 };
 
 // LDS layout (bytes)
@@ -89,6 +91,8 @@ struct PlArgs {
   int64_t cache_bs, cache_hs;
   const int32_t* pad;
   const int32_t* tstate;
+  const int32_t* kv_rows;  // beams: [R][ld_rows] cache row of each prefix position, else null
+  int64_t ld_rows;
   int kv_base, kstep, R, layer, last;
   float eps;
   unsigned char* scratch;
@@ -135,6 +139,7 @@ __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uin
   }
 }
 
+template <int MT, bool ROWS>
 __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   typedef __attribute__((address_space(3))) void lds_void;
@@ -159,37 +164,40 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   float* mu = rsq + 8 * 32;
   float* rsd = mu + 32;
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
-  constexpr bool compute = true;  // (every wave computes; kept as a name for the phase guards)
+  uint16_t* obf = reinterpret_cast<uint16_t*>(smem + L_OBF);  // o staging [2][64], then f tiles [32][16]
   const int R = p.R;
   if (tid == 0) *abort_flag = 0;
 
-  // ---- (A0) compute waves: c_attn operands first (weights nt, 12 of 16 fragment columns real; A = x^
-  // rows 0..31), then the attention's first round of K/V rows, then this tile's residual slice
   const int w = wave;
-  const int c16 = lane & 15, q4 = lane >> 4;
+  const int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
   const int kidx = p.kv_base + p.tstate[0] + p.kstep;
-  u32x4_t bw[4] = {}, av[4][2] = {};
-  const int u = w >> 2;                                  // attention unit of this wave (rows 2jj + u)
-  const int r_u = 2 * jj + u;
-  const bool act_u = r_u < R;
-  const int rr = act_u ? r_u : 0;
+  // attention: this workgroup's rows of head h are 32 pt + 2 jj + u (pass pt, unit u = waves 4u .. 4u+3)
+  const int u = w >> 2;
   const int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
   constexpr int NG = 32;
-  const int p0 = p.pad ? p.pad[rr] : 0;
-  const int nk = kidx + 1 - p0;
-  const uint16_t* Kc = p.kc + (int64_t)rr * p.cache_bs + (int64_t)h * p.cache_hs;
-  const uint16_t* Vc = p.vc + (int64_t)rr * p.cache_bs + (int64_t)h * p.cache_hs;
   u32x4_t kr[kKB], vr[kKB];
-  auto kv_load = [&](u32x4_t (&dst)[kKB], const uint16_t* base, int j0) {
+  // K/V rows of key index jk (0-based from the row's first valid key) of row `row`: the row's own cache
+  // row, or (beams) the row of kv_rows[row][position] that holds that prefix position
+  auto kv_ptr = [&](const uint16_t* cache, int row, int pos) -> const uint16_t* {
+    int crow = row;
+    if constexpr (ROWS) crow = p.kv_rows[(int64_t)row * p.ld_rows + pos];
+    return cache + (int64_t)crow * p.cache_bs + (int64_t)h * p.cache_hs + (int64_t)pos * kHD + 8 * d8;
+  };
+  auto kv_load = [&](u32x4_t (&dst)[kKB], const uint16_t* cache, int row, int p0, int nk, int j0) {
 #pragma unroll
     for (int uu = 0; uu < kKB; ++uu) {
       const int jk = min(j0 + NG * uu + g, max(nk - 2, 0));
-      dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(base + (int64_t)(p0 + jk) * kHD + 8 * d8));
+      dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk)));
     }
   };
-  const int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns
-  float2 x_old = {0.f, 0.f};
-  if (compute) {
+  auto unit_row = [&](int pt) { return 32 * pt + 2 * jj + u; };
+  const int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns per tile
+
+  // ---- (A0) c_attn operands first (weights nt, 12 of 16 fragment columns real; A = x^ tile 0), then the
+  // attention's first round of K/V rows (pass 0), then the residual slices, then the weight DMA
+  u32x4_t bw[4], av[4][2];
+  float2 x_old[MT];
+  {
     const u32x4_t* wq = p.qkv_w12 + (int64_t)b * 32 * 4 * kQC;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -200,11 +208,18 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
     }
     __builtin_amdgcn_sched_barrier(0);
-    kv_load(kr, Kc, 0);
-    kv_load(vr, Vc, 0);
-    const int xr = xrow < R ? xrow : R - 1;
-    const float2 xv = *reinterpret_cast<const float2*>(p.x + (int64_t)xr * kD + xcol);
-    x_old = xrow < R ? xv : float2{0.f, 0.f};
+    {
+      const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
+      const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+      kv_load(kr, p.kc, rr, p0, nk, 0);
+      kv_load(vr, p.vc, rr, p0, nk, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int row = 32 * t + xrow, xr = row < R ? row : R - 1;
+      const float2 xv = *reinterpret_cast<const float2*>(p.x + (int64_t)xr * kD + xcol);
+      x_old[t] = row < R ? xv : float2{0.f, 0.f};
+    }
     __builtin_amdgcn_sched_barrier(0);
     // this workgroup's attn.c_proj (8 KiB), c_fc (32 KiB), mlp.c_proj (32 KiB) weight slices, global ->
     // LDS by DMA (1 KiB per wave instruction, lane-linear = fragment order, nt), instruction t by wave t % 8
@@ -227,29 +242,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
   }
 
-  // ---- (A) c_attn: decode_gemm16x FOLD arithmetic (k-steps w + 8i, row statistics from the A fragments)
-  f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
-  float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
-  if (compute) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&bw[i]);
-      const bf16x8_t bz = c16 < kQC ? bfr : bf16x8_t{};
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&av[i][t]);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, acc[t], 0, 0, 0);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = (float)a[e];
-          ssum[t] += v;
-          ssq[t] = fmaf(v, v, ssq[t]);
-        }
-      }
-    }
+  // fold statistics of one 32-row tile (the A fragments a wave accumulated): sums -> mu / rstd in LDS
+  auto fold_stats = [&](const float (&ss)[2], const float (&sq)[2]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      float a = ssum[t], s2 = ssq[t];
+      float a = ss[t], s2 = sq[t];
       a += __shfl_xor(a, 16, 64);
       a += __shfl_xor(a, 32, 64);
       s2 += __shfl_xor(s2, 16, 64);
@@ -258,45 +255,84 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         rsum[w * 32 + 16 * t + c16] = a;
         rsq[w * 32 + 16 * t + c16] = s2;
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[(w * 8 + 4 * t + r) * 64 + lane] = acc[t][r];
     }
-  }
-  bar();
-  if (tid < 32) {
-    float S = 0.f, Q = 0.f;
+  };
+  auto mu_rs = [&]() {
+    if (tid < 32) {
+      float S = 0.f, Q = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < kNW; ++ww) {
-      S += rsum[ww * 32 + tid];
-      Q += rsq[ww * 32 + tid];
+      for (int ww = 0; ww < kNW; ++ww) {
+        S += rsum[ww * 32 + tid];
+        Q += rsq[ww * 32 + tid];
+      }
+      const float inv = 1.0f / kD, m = S * inv;
+      mu[tid] = m;
+      rsd[tid] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
     }
-    const float inv = 1.0f / kD, m = S * inv;
-    mu[tid] = m;
-    rsd[tid] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
-  }
-  bar();
-  if (compute) {  // one output per thread: 32 rows x 16 fragment columns (12 real)
-    const int e = tid >> 6, l = lane, col = l & 15;
-    if (col < kQC) {
-      float v = 0.f;
+  };
+
+  // ---- (A) c_attn per 32-row tile: decode_gemm16x FOLD arithmetic (k-steps w + 8i, statistics from the
+  // A fragments); q / k / v of row r, head h -> granules gq[r][h][192]; this step's k / v into the cache
+#pragma unroll 1
+  for (int t = 0; t < MT; ++t) {
+    if (t > 0) {
 #pragma unroll
-      for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
-      const int row = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
-      const float* uc = p.qkv_uc + (int64_t)b * 2 * kQC;
-      v = rsd[row] * (v - mu[row] * uc[col]);
-      v += uc[kQC + col];
-      const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
-      const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
-      __hip_atomic_store(gq + ((int64_t)h * 32 + row) * 192 + i, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (i >= kHD && row < R) {  // this step's key / value into the cache (attention kernel: 0 + v, rounded)
-        uint16_t* dst = (i < 2 * kHD ? p.kc : p.vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
-                        (int64_t)kidx * kHD + (i & (kHD - 1));
-        *dst = f2bf(0.f + v);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+          av[i][hf] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4);
+    }
+    f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+    float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&bw[i]);
+      const bf16x8_t bz = c16 < kQC ? bfr : bf16x8_t{};
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&av[i][hf]);
+        acc[hf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, acc[hf], 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = (float)a[e];
+          ssum[hf] += v;
+          ssq[hf] = fmaf(v, v, ssq[hf]);
+        }
       }
     }
+    fold_stats(ssum, ssq);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(w * 8 + 4 * hf + r) * 64 + lane] = acc[hf][r];
+    bar();
+    mu_rs();
+    bar();
+    {  // one output per thread: 32 rows x 16 fragment columns (12 real)
+      const int e = tid >> 6, l = lane, col = l & 15;
+      if (col < kQC) {
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
+        const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = 32 * t + rt;
+        const float* uc = p.qkv_uc + (int64_t)b * 2 * kQC;
+        v = rsd[rt] * (v - mu[rt] * uc[col]);
+        v += uc[kQC + col];
+        const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
+        const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
+        __hip_atomic_store(gq + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i >= kHD && row < R) {  // this step's key / value into the row's own cache row (0 + v, rounded)
+          uint16_t* dst = (i < 2 * kHD ? p.kc : p.vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
+                          (int64_t)kidx * kHD + (i & (kHD - 1));
+          *dst = f2bf(0.f + v);
+        }
+      }
+    }
+    if (MT > 1) bar();  // red / statistics are reused by the next tile
   }
 
-  // ---- (E1 + B) attention, unit u = rows 2jj + u of head h, waves 4u .. 4u+3
+  // ---- (E1 + B) attention passes: unit u of pass pt = row 32 pt + 2 jj + u of head h (attn_decode_kernel
+  // algorithm: 32 groups x 8 lanes, keys g + 32 n, fixed kSub-key softmax chunks, fixed-order merge)
   unsigned char* ub = smem + L_ATT + u * ((kUnitBytes + 15) / 16 * 16);
   float* qs = reinterpret_cast<float*>(ub);
   float* kn = qs + kHD;
@@ -304,172 +340,168 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   float* gm = vn + kHD;
   float* gl = gm + 32;
   float* pv = gl + 32;
-  float* ofin = pv + kPvRows * kPvPitch;
-  if (compute && (w & 3) == 0 && act_u) {  // the unit's first wave sweeps its 192 granules
-    const uint64_t* src = gq + ((int64_t)h * 32 + r_u) * 192;
-    uint64_t g0, g1, g2;
-    bool ok = false;
-    for (uint32_t n = 0;; ++n) {
-      g0 = ld_sc1_u64(src + lane);
-      g1 = ld_sc1_u64(src + 64 + lane);
-      g2 = ld_sc1_u64(src + 128 + lane);
-      const bool mine = (uint32_t)(g0 >> 32) == L1 && (uint32_t)(g1 >> 32) == L1 && (uint32_t)(g2 >> 32) == L1;
-      if (__all(mine)) {
-        ok = true;
-        break;
-      }
-      if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err) != 0)) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ok) {
-      if (lane == 0) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *abort_flag = 1;
-      }
-    } else {
-      qs[lane] = (0.f + __uint_as_float((uint32_t)g0)) * 0.125f;  // 1/sqrt(64), exact
-      kn[lane] = 0.f + __uint_as_float((uint32_t)g1);
-      vn[lane] = 0.f + __uint_as_float((uint32_t)g2);
-    }
-  }
-  bar();
-  if (*abort_flag) return;
-  float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
-  if (compute && act_u) {
-    float q[8], kme[8], vme[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      q[e] = qs[8 * d8 + e];
-      kme[e] = kn[8 * d8 + e];
-      vme[e] = vn[8 * d8 + e];
-    }
-    auto unpack = [&](const u32x4_t& r, float (&xv)[8]) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        xv[2 * i] = __uint_as_float(r[i] << 16);
-        xv[2 * i + 1] = __uint_as_float(r[i] & 0xFFFF0000u);
-      }
-    };
-    for (int j0 = 0; j0 < nk; j0 += NG * kKB) {
-      const bool more = j0 + NG * kKB < nk;
-      float s[kKB];
-#pragma unroll
-      for (int uu = 0; uu < kKB; ++uu) {
-        const int jk = j0 + NG * uu + g;
-        float kx[8];
-        unpack(kr[uu], kx);
-        if (jk >= nk - 1) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) kx[e] = kme[e];
-        }
-        float pt = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) pt = fmaf(q[e], kx[e], pt);
-        pt = sum8_dpp(pt);
-        s[uu] = jk < nk ? pt : -INFINITY;
-      }
-      if (more) kv_load(kr, Kc, j0 + NG * kKB);
-#pragma unroll
-      for (int c0 = 0; c0 < kKB; c0 += kSub) {
-        float bm = -INFINITY;
-#pragma unroll
-        for (int uu = c0; uu < c0 + kSub; ++uu) bm = fmaxf(bm, s[uu]);
-        if (bm == -INFINITY) continue;
-        const float mn = fmaxf(m_run, bm);
-        const float corr = __expf(m_run - mn);
-        l_run *= corr;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o8[e] *= corr;
-#pragma unroll
-        for (int uu = c0; uu < c0 + kSub; ++uu) {
-          const int jk = j0 + NG * uu + g;
-          const float pr = __expf(s[uu] - mn);
-          l_run += pr;
-          float vx[8];
-          unpack(vr[uu], vx);
-          if (jk >= nk - 1) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) vx[e] = vme[e];
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o8[e] = fmaf(pr, vx[e], o8[e]);
-        }
-        m_run = mn;
-      }
-      if (more) kv_load(vr, Vc, j0 + NG * kKB);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
-    if (d8 == 0) {
-      gm[g] = m_run;
-      gl[g] = l_run;
-    }
-  }
-  bar();
   constexpr int NQ = 4, GPQ = 8;
   float* qsum = pv + 32 * kPvPitch;
   float* lsum = qsum + NQ * kPvPitch;
-  if (compute && act_u) {
-    const int dd = tu & (kHD - 1), qd = tu / kHD;
-    float M = -INFINITY;
-#pragma unroll 8
-    for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
-    float Ls = 0.f, a = 0.f;
-#pragma unroll
-    for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
-      const float wgt = __expf(gm[i] - M);
-      Ls = fmaf(gl[i], wgt, Ls);
-      a = fmaf(pv[i * kPvPitch + dd], wgt, a);
+  auto rsrc_ob = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x7fffffff, 0x00020000);
+#pragma unroll 1
+  for (int pt = 0; pt < MT; ++pt) {
+    const int r_u = unit_row(pt);
+    const bool act_u = r_u < R;
+    const int rr = act_u ? r_u : 0;
+    const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+    if (pt > 0) {  // later passes: this pass's first round now
+      kv_load(kr, p.kc, rr, p0, nk, 0);
+      kv_load(vr, p.vc, rr, p0, nk, 0);
     }
-    qsum[qd * kPvPitch + dd] = a;
-    if (dd == 0) lsum[qd] = Ls;
-  }
-  bar();
-  uint16_t* obf = reinterpret_cast<uint16_t*>(smem + L_OBF);
-  if (compute && tu < kHD) {
-    float v = 0.f;
+    if ((w & 3) == 0 && act_u) {  // the unit's first wave sweeps its 192 granules
+      const uint64_t* src = gq + ((int64_t)r_u * kH + h) * 192;
+      uint64_t g0, g1, g2;
+      bool ok = false;
+      for (uint32_t n = 0;; ++n) {
+        g0 = ld_sc1_u64(src + lane);
+        g1 = ld_sc1_u64(src + 64 + lane);
+        g2 = ld_sc1_u64(src + 128 + lane);
+        const bool mine = (uint32_t)(g0 >> 32) == L1 && (uint32_t)(g1 >> 32) == L1 && (uint32_t)(g2 >> 32) == L1;
+        if (__all(mine)) {
+          ok = true;
+          break;
+        }
+        if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err) != 0)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!ok) {
+        if (lane == 0) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *abort_flag = 1;
+        }
+      } else {
+        qs[lane] = (0.f + __uint_as_float((uint32_t)g0)) * 0.125f;  // 1/sqrt(64), exact
+        kn[lane] = 0.f + __uint_as_float((uint32_t)g1);
+        vn[lane] = 0.f + __uint_as_float((uint32_t)g2);
+      }
+    }
+    bar();
+    if (*abort_flag) return;
     if (act_u) {
+      float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      float m_run = -INFINITY, l_run = 0.f;
+      float q[8], kme[8], vme[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        q[e] = qs[8 * d8 + e];
+        kme[e] = kn[8 * d8 + e];
+        vme[e] = vn[8 * d8 + e];
+      }
+      auto unpack = [&](const u32x4_t& r, float (&xv)[8]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          xv[2 * i] = __uint_as_float(r[i] << 16);
+          xv[2 * i + 1] = __uint_as_float(r[i] & 0xFFFF0000u);
+        }
+      };
+      for (int j0 = 0; j0 < nk; j0 += NG * kKB) {
+        const bool more = j0 + NG * kKB < nk;
+        float sc[kKB];
+#pragma unroll
+        for (int uu = 0; uu < kKB; ++uu) {
+          const int jk = j0 + NG * uu + g;
+          float kx[8];
+          unpack(kr[uu], kx);
+          if (jk >= nk - 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) kx[e] = kme[e];
+          }
+          float pt_ = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pt_ = fmaf(q[e], kx[e], pt_);
+          pt_ = sum8_dpp(pt_);
+          sc[uu] = jk < nk ? pt_ : -INFINITY;
+        }
+        if (more) kv_load(kr, p.kc, rr, p0, nk, j0 + NG * kKB);
+#pragma unroll
+        for (int c0 = 0; c0 < kKB; c0 += kSub) {
+          float bm = -INFINITY;
+#pragma unroll
+          for (int uu = c0; uu < c0 + kSub; ++uu) bm = fmaxf(bm, sc[uu]);
+          if (bm == -INFINITY) continue;
+          const float mn = fmaxf(m_run, bm);
+          const float corr = __expf(m_run - mn);
+          l_run *= corr;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o8[e] *= corr;
+#pragma unroll
+          for (int uu = c0; uu < c0 + kSub; ++uu) {
+            const int jk = j0 + NG * uu + g;
+            const float pr = __expf(sc[uu] - mn);
+            l_run += pr;
+            float vx[8];
+            unpack(vr[uu], vx);
+            if (jk >= nk - 1) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) vx[e] = vme[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o8[e] = fmaf(pr, vx[e], o8[e]);
+          }
+          m_run = mn;
+        }
+        if (more) kv_load(vr, p.vc, rr, p0, nk, j0 + NG * kKB);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
+      if (d8 == 0) {
+        gm[g] = m_run;
+        gl[g] = l_run;
+      }
+    }
+    bar();
+    if (act_u) {
+      const int dd = tu & (kHD - 1), qd = tu / kHD;
+      float M = -INFINITY;
+#pragma unroll 8
+      for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
       float Ls = 0.f, a = 0.f;
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        Ls += lsum[i];
-        a += qsum[i * kPvPitch + tu];
+      for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
+        const float wgt = __expf(gm[i] - M);
+        Ls = fmaf(gl[i], wgt, Ls);
+        a = fmaf(pv[i * kPvPitch + dd], wgt, a);
       }
-      v = a / Ls;
+      qsum[qd * kPvPitch + dd] = a;
+      if (dd == 0) lsum[qd] = Ls;
     }
-    obf[u * kHD + tu] = f2bf(v);
-  }
-  bar();
-  if (compute && (tu & 0xff) < 8) {  // o rows -> the cluster's [32][128] tile, write-through 16-B stores
-    const int d0 = 8 * (tu & 7);
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
-    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, ((c * 32 + r_u) * 128 + hh * kHD + d0) * 2, 0, 16);
+    bar();
+    if (tu < kHD) {
+      float v = 0.f;
+      if (act_u) {
+        float Ls = 0.f, a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+          Ls += lsum[i];
+          a += qsum[i * kPvPitch + tu];
+        }
+        v = a / Ls;
+      }
+      obf[u * kHD + tu] = f2bf(v);
+    }
+    bar();
+    if (tu < 8) {  // o rows -> the cluster's [rows][128] tile, write-through 16-B stores
+      const int d0 = 8 * tu;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_ob, ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, 16);
+    }
+    if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
   drain();  // the o stores, and this wave's weight DMA (read from LDS from phase C on)
   bar();
   if (tid == 0) add_relaxed(cnt + CNT2 + c);
 
-  // ---- (C) attn.c_proj split c, tile j: decode_gemm_kernel EPI 2 arithmetic (one 16-deep k-step per wave)
+  // ---- (C) attn.c_proj split c, tile j, per 32-row tile: decode_gemm_kernel EPI 2 (one k-step per wave)
   if (tid == 0 && !poll_ge(cnt + CNT2 + c, kCPC * L1, err, 2)) *abort_flag = 1;
   bar();
   if (*abort_flag) return;
-  const int r32 = lane & 31, hb = lane >> 5;
-  if (compute) {
-    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x7fffffff, 0x00020000);
-    const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((c * 32 + r32) * 128 + 16 * w + 8 * hb) * 2, 0, 16);
-    const u32x4_t bb = *reinterpret_cast<const u32x4_t*>(smem + L_WO + w * 1024 + lane * 16);
-    f32x16_t acc32;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
-    acc32 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t*>(&a),
-                                                    *reinterpret_cast<const bf16x8_t*>(&bb), acc32, 0, 0, 0);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
-  }
-  bar();
-  auto store_partial = [&](float* dst) {  // 1024 outputs, 2 per thread; fixed-order sum over the waves
+  auto store_partial = [&](float* dst, int t) {  // 1024 outputs of row tile t, 2 per thread, fixed-order sum
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int o = tid + 512 * k;
@@ -477,14 +509,30 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
       for (int ww = 0; ww < kNW; ++ww) v += red[ww * 1024 + o];
       const int r = o >> 6, l = o & 63;
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-      st_sc1_u32(reinterpret_cast<uint32_t*>(dst + ((int64_t)c * 32 + row) * kD + 32 * j + (l & 31)), __float_as_uint(v));
+      const int row = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      st_sc1_u32(reinterpret_cast<uint32_t*>(dst + ((int64_t)c * kMaxR + row) * kD + 32 * j + (l & 31)),
+                 __float_as_uint(v));
     }
   };
-  if (compute) {
-    store_partial(p1);
-    drain();
+  {
+    const u32x4_t bb = *reinterpret_cast<const u32x4_t*>(smem + L_WO + w * 1024 + lane * 16);
+#pragma unroll 1
+    for (int t = 0; t < MT; ++t) {
+      const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(
+          rsrc_ob, ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, 16);
+      f32x16_t acc32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
+      acc32 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t*>(&a),
+                                                      *reinterpret_cast<const bf16x8_t*>(&bb), acc32, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
+      bar();
+      store_partial(p1, t);
+      bar();
+    }
   }
+  drain();
   bar();
   if (tid == 0) add_relaxed(cnt + CNT3 + j);
 
@@ -492,154 +540,158 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   if (tid == 0 && !poll_ge(cnt + CNT3 + j, kNC * L1, err, 3)) *abort_flag = 1;
   bar();
   if (*abort_flag) return;
-  float2 x1 = {0.f, 0.f};
-  if (compute) {
-    float2 pp = *reinterpret_cast<const float2*>(p.o_b + xcol);
+  float2 x1[MT];
+  {
+    const float2 ob2 = *reinterpret_cast<const float2*>(p.o_b + xcol);
 #pragma unroll
-    for (int cc = 0; cc < kNC; ++cc) {
-      const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p1 + ((int64_t)cc * 32 + xrow) * kD + xcol));
-      pp.x += __uint_as_float((uint32_t)v);
-      pp.y += __uint_as_float((uint32_t)(v >> 32));
+    for (int t = 0; t < MT; ++t) {
+      const int row = 32 * t + xrow;
+      float2 pp = ob2;
+#pragma unroll
+      for (int cc = 0; cc < kNC; ++cc) {
+        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p1 + ((int64_t)cc * kMaxR + row) * kD + xcol));
+        pp.x += __uint_as_float((uint32_t)v);
+        pp.y += __uint_as_float((uint32_t)(v >> 32));
+      }
+      x1[t] = float2{x_old[t].x + pp.x, x_old[t].y + pp.y};
+      st_sc1_u32(reinterpret_cast<uint32_t*>(xc + (((int64_t)c * kMaxR + row) * kD + xcol) * 2),
+                 pack2bf(x1[t].x, x1[t].y));
     }
-    x1 = float2{x_old.x + pp.x, x_old.y + pp.y};
-    st_sc1_u32(reinterpret_cast<uint32_t*>(xc + (((int64_t)c * 32 + xrow) * kD + xcol) * 2), pack2bf(x1.x, x1.y));
-    drain();
   }
+  drain();
   bar();
   if (tid == 0) add_relaxed(cnt + CNT4 + c);
 
-  // ---- (E) c_fc (ln_2 folded) + gelu on tile 32c + j, A = the cluster's x1^ (decode_gemm16x FOLD)
+  // ---- (E) c_fc (ln_2 folded) + gelu on column tile 32c + j, per row tile, A = the cluster's x1^
   if (tid == 0 && !poll_ge(cnt + CNT4 + c, kCPC * L1, err, 4)) *abort_flag = 1;
   bar();
   if (*abort_flag) return;
-  if (compute) {
+  {
     auto rsrc = __builtin_amdgcn_make_buffer_rsrc(xc, 0, 0x7fffffff, 0x00020000);
-    u32x4_t ax[4][2];
+    auto rsrc_f = __builtin_amdgcn_make_buffer_rsrc(fcb, 0, 0x7fffffff, 0x00020000);
+#pragma unroll 1
+    for (int t = 0; t < MT; ++t) {
+      u32x4_t ax[4][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        ax[i][t] = __builtin_amdgcn_raw_buffer_load_b128(
-            rsrc, ((c * 32 + 16 * t + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, 16);
-    f32x4_t af[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
-    float fs[2] = {0.f, 0.f}, fq[2] = {0.f, 0.f};
+        for (int hf = 0; hf < 2; ++hf)
+          ax[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
+              rsrc, ((c * kMaxR + 32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, 16);
+      f32x4_t af[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+      float fs[2] = {0.f, 0.f}, fq[2] = {0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(smem + L_WFC + (w + 8 * i) * 1024 + lane * 16);
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(smem + L_WFC + (w + 8 * i) * 1024 + lane * 16);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&ax[i][t]);
-        af[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, af[t], 0, 0, 0);
+        for (int hf = 0; hf < 2; ++hf) {
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&ax[i][hf]);
+          af[hf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, af[hf], 0, 0, 0);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = (float)a[e];
-          fs[t] += v;
-          fq[t] = fmaf(v, v, fq[t]);
+          for (int e = 0; e < 8; ++e) {
+            const float v = (float)a[e];
+            fs[hf] += v;
+            fq[hf] = fmaf(v, v, fq[hf]);
+          }
         }
       }
-    }
+      fold_stats(fs, fq);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float a = fs[t], s2 = fq[t];
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (q4 == 0) {
-        rsum[w * 32 + 16 * t + c16] = a;
-        rsq[w * 32 + 16 * t + c16] = s2;
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(w * 8 + 4 * hf + r) * 64 + lane] = af[hf][r];
+      bar();
+      mu_rs();
+      bar();
+      {
+        const int e = tid >> 6, l = lane;
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
+        const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
+        const int n = (32 * c + j) * 16 + (l & 15);
+        v = rsd[rt] * (v - mu[rt] * p.fc_u[n]);
+        v += p.fc_c[n];
+        v = gelu_tanh_pl(v);
+        obf[rt * 16 + (l & 15)] = f2bf(v);
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[(w * 8 + 4 * t + r) * 64 + lane] = af[t][r];
+      bar();
+      if (tid < 64) {  // [32 rows][16 columns] bf16 -> the cluster's f tile, write-through 16-B stores
+        const int rt = tid >> 1, half = tid & 1;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + rt * 16 + 8 * half);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_f, ((c * kMaxR + 32 * t + rt) * 512 + 16 * j + 8 * half) * 2,
+                                               0, 16);
+      }
+      if (MT > 1) bar();
     }
   }
-  bar();
-  if (tid < 32) {
-    float S = 0.f, Q = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < kNW; ++ww) {
-      S += rsum[ww * 32 + tid];
-      Q += rsq[ww * 32 + tid];
-    }
-    const float inv = 1.0f / kD, m = S * inv;
-    mu[tid] = m;
-    rsd[tid] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
-  }
-  bar();
-  uint16_t* ftile = obf;  // [32][16] bf16 (the o staging is consumed)
-  if (compute) {
-    const int e = tid >> 6, l = lane;
-    float v = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
-    const int row = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
-    const int n = (32 * c + j) * 16 + (l & 15);
-    v = rsd[row] * (v - mu[row] * p.fc_u[n]);
-    v += p.fc_c[n];
-    v = gelu_tanh_pl(v);
-    ftile[row * 16 + (l & 15)] = f2bf(v);
-  }
-  bar();
-  if (tid < 64) {  // [32 rows][16 columns] bf16 -> the cluster's f tile, write-through 16-B stores
-    const int row = tid >> 1, half = tid & 1;
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(ftile + row * 16 + 8 * half);
-    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(fcb, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, ((c * 32 + row) * 512 + 16 * j + 8 * half) * 2, 0, 16);
-    drain();
-  }
+  drain();
   bar();
   if (tid == 0) add_relaxed(cnt + CNT5 + c);
 
-  // ---- (F) mlp.c_proj split c, tile j: decode_gemm_kernel EPI 2 (k-steps w + 8i of the split)
+  // ---- (F) mlp.c_proj split c, tile j, per row tile: decode_gemm_kernel EPI 2 (k-steps w + 8i of the split)
   if (tid == 0 && !poll_ge(cnt + CNT5 + c, kCPC * L1, err, 5)) *abort_flag = 1;
   bar();
   if (*abort_flag) return;
-  if (compute) {
+  {
     auto rsrc = __builtin_amdgcn_make_buffer_rsrc(fcb, 0, 0x7fffffff, 0x00020000);
-    u32x4_t a4[4];
+#pragma unroll 1
+    for (int t = 0; t < MT; ++t) {
+      u32x4_t a4[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      a4[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((c * 32 + r32) * 512 + 16 * (w + 8 * i) + 8 * hb) * 2, 0, 16);
-    f32x16_t acc32;
+      for (int i = 0; i < 4; ++i)
+        a4[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            rsrc, ((c * kMaxR + 32 * t + r32) * 512 + 16 * (w + 8 * i) + 8 * hb) * 2, 0, 16);
+      f32x16_t acc32;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      acc32 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-          *reinterpret_cast<const bf16x8_t*>(&a4[i]),
-          *reinterpret_cast<const bf16x8_t*>(smem + L_WPJ + (w + 8 * i) * 1024 + lane * 16), acc32, 0, 0, 0);
+      for (int i = 0; i < 4; ++i)
+        acc32 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            *reinterpret_cast<const bf16x8_t*>(&a4[i]),
+            *reinterpret_cast<const bf16x8_t*>(smem + L_WPJ + (w + 8 * i) * 1024 + lane * 16), acc32, 0, 0, 0);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
+      for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
+      bar();
+      store_partial(p2, t);
+      bar();
+    }
   }
-  bar();
-  if (compute) {
-    store_partial(p2);
-    drain();
-  }
+  drain();
   bar();
   if (tid == 0) add_relaxed(cnt + CNT6 + j);
 
-  // ---- (G) x2 = x1 + (b_proj + sum_c partial_c); x, x^ for the next launch (cluster c: rows 4c .. 4c+3)
-  // The last layer stores x1 and leaves this reduce (with ln_f + final_norm, Q5) to itts_residual_reduce_ln.
+  // ---- (G) x2 = x1 + (b_proj + sum_c partial_c); x, x^ for the next launch (cluster c: rows 4c .. 4c+3 of
+  // every tile).  The last layer stores x1 and leaves this reduce (with ln_f + final_norm, Q5) to
+  // itts_residual_reduce_ln over the partials.
   if (p.last) {
-    if (compute && (xrow >> 2) == c && xrow < R)
-      *reinterpret_cast<float2*>(p.x + (int64_t)xrow * kD + xcol) = x1;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int row = 32 * t + xrow;
+      if ((xrow >> 2) == c && row < R) *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x1[t];
+    }
     return;
   }
   if (tid == 0 && !poll_ge(cnt + CNT6 + j, kNC * L1, err, 6)) *abort_flag = 1;
   bar();
   if (*abort_flag) return;
-  if (compute && (xrow >> 2) == c && xrow < R) {
-    float2 pp = *reinterpret_cast<const float2*>(p.proj_b + xcol);
+  if ((xrow >> 2) == c) {
+    const float2 pb2 = *reinterpret_cast<const float2*>(p.proj_b + xcol);
 #pragma unroll
-    for (int cc = 0; cc < kNC; ++cc) {
-      const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p2 + ((int64_t)cc * 32 + xrow) * kD + xcol));
-      pp.x += __uint_as_float((uint32_t)v);
-      pp.y += __uint_as_float((uint32_t)(v >> 32));
+    for (int t = 0; t < MT; ++t) {
+      const int row = 32 * t + xrow;
+      if (row >= R) continue;
+      float2 pp = pb2;
+#pragma unroll
+      for (int cc = 0; cc < kNC; ++cc) {
+        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p2 + ((int64_t)cc * kMaxR + row) * kD + xcol));
+        pp.x += __uint_as_float((uint32_t)v);
+        pp.y += __uint_as_float((uint32_t)(v >> 32));
+      }
+      const float2 x2 = float2{x1[t].x + pp.x, x1[t].y + pp.y};
+      *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x2;
+      *reinterpret_cast<uint32_t*>(p.xh + (int64_t)row * kD + xcol) = pack2bf(x2.x, x2.y);
     }
-    const float2 x2 = float2{x1.x + pp.x, x1.y + pp.y};
-    *reinterpret_cast<float2*>(p.x + (int64_t)xrow * kD + xcol) = x2;
-    *reinterpret_cast<uint32_t*>(p.xh + (int64_t)xrow * kD + xcol) = pack2bf(x2.x, x2.y);
   }
 }
 
@@ -650,7 +702,7 @@ int g_cu_count = -1;
 extern "C" int64_t itts_gpt_pl_scratch_bytes(void) { return kScratchBytes; }
 
 extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
-  if (!w || w->d_model != kD || w->n_head != kH || rows < 1 || rows > 32) return 0;
+  if (!w || w->d_model != kD || w->n_head != kH || rows < 1 || rows > kMaxR) return 0;
   if (g_cu_count < 0) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -680,7 +732,8 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   ITTS_REQUIRE(pl->qkv_w12 && pl->qkv_uc && ly->o_w && ly->fc_w16 && ly->fc_u && ly->fc_c && ly->proj_w &&
                    ly->proj_b && ly->o_c,
                fn, "incomplete layer weights");
-  ITTS_REQUIRE(st->rows >= 1 && st->rows <= 32 && !st->kv_rows, fn, "1..32 rows, no beam lineage");
+  ITTS_REQUIRE(st->rows >= 1 && st->rows <= kMaxR, fn, "1..128 rows");
+  ITTS_REQUIRE(!st->kv_rows || st->ld_rows >= st->max_kv, fn, "kv_rows [rows][ld_rows >= max_kv]");
   ITTS_REQUIRE(st->x && st->xh && st->k_cache && st->v_cache && st->tstate, fn, "null state buffer");
   ITTS_REQUIRE((reinterpret_cast<uintptr_t>(scratch) & 255) == 0, fn, "scratch must be 256-B aligned");
   const int64_t cache_hs = (int64_t)st->max_kv * kHD, cache_bs = (int64_t)kH * cache_hs;
@@ -703,6 +756,8 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   a.cache_hs = cache_hs;
   a.pad = st->pad;
   a.tstate = st->tstate;
+  a.kv_rows = st->kv_rows;
+  a.ld_rows = st->ld_rows;
   a.kv_base = st->kv_base;
   a.kstep = kstep;
   a.R = st->rows;
@@ -710,18 +765,40 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   a.last = last;
   a.eps = 1e-5f;
   a.scratch = static_cast<unsigned char*>(scratch);
-  static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(gpt_layer_pl_kernel),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) == hipSuccess;
-  ITTS_REQUIRE(lds_ok, fn, "cannot reserve the kernel's LDS");
-  hipLaunchKernelGGL(gpt_layer_pl_kernel, dim3(kWG), dim3(kThreads), kLdsBytes, itts::as_stream(stream), a);
+  const int mt = (st->rows + 31) / 32;
+  const void* fnp = nullptr;
+#define PL_K(MTV, RW) reinterpret_cast<const void*>(gpt_layer_pl_kernel<MTV, RW>)
+  switch (mt) {
+    case 1: fnp = st->kv_rows ? PL_K(1, true) : PL_K(1, false); break;
+    case 2: fnp = st->kv_rows ? PL_K(2, true) : PL_K(2, false); break;
+    case 3: fnp = st->kv_rows ? PL_K(3, true) : PL_K(3, false); break;
+    default: fnp = st->kv_rows ? PL_K(4, true) : PL_K(4, false); break;
+  }
+#undef PL_K
+  static bool lds_ok[8] = {};
+  const int ki = 2 * (mt - 1) + (st->kv_rows ? 1 : 0);
+  if (!lds_ok[ki])
+    lds_ok[ki] = hipFuncSetAttribute(fnp, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) == hipSuccess;
+  ITTS_REQUIRE(lds_ok[ki], fn, "cannot reserve the kernel's LDS");
+  hipStream_t s = itts::as_stream(stream);
+  switch (ki) {
+    case 0: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+    case 1: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, true>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+    case 2: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, false>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+    case 3: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, true>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+    case 4: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, false>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+    case 5: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, true>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+    case 6: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, false>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+    default: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, true>), dim3(kWG), dim3(kThreads), kLdsBytes, s, a); break;
+  }
   return itts::check_launch(fn);
 }
 
-// zero the step's counters and granules (one memset node ahead of the layer launches)
-extern "C" int itts_gpt_pl_begin_step(void* scratch, void* stream) {
+// zero the step's counters and the granules of its rows (one memset node ahead of the layer launches)
+extern "C" int itts_gpt_pl_begin_step(void* scratch, int rows, void* stream) {
   const char* fn = "itts_gpt_pl_begin_step";
-  ITTS_REQUIRE(scratch, fn, "null pointer");
-  if (hipMemsetAsync(scratch, 0, kZeroBytes, itts::as_stream(stream)) != hipSuccess) return itts::check_launch(fn);
+  ITTS_REQUIRE(scratch && rows >= 1 && rows <= kMaxR, fn, "null scratch or rows outside 1..128");
+  if (hipMemsetAsync(scratch, 0, zero_bytes(rows), itts::as_stream(stream)) != hipSuccess) return itts::check_launch(fn);
   return 0;
 }
 
@@ -731,22 +808,24 @@ extern "C" int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPl
   const char* fn = "itts_gpt_decode_steps_pl";
   ITTS_REQUIRE(w && pl && scratch && st && smp && w->layers, fn, "null pointer");
   ITTS_REQUIRE(nsteps >= 1 && nsteps <= 64, fn, "nsteps must be in [1, 64]");
-  ITTS_REQUIRE(smp->mode == 0 || smp->mode == 1, fn, "greedy / sampling only (beams: itts_gpt_decode_step)");
+  ITTS_REQUIRE(smp->mode >= 0 && smp->mode <= 2, fn, "sampling mode must be 0, 1 or 2");
+  ITTS_REQUIRE(nsteps == 1 || smp->mode != 2, fn, "beam decoding (mode 2) runs one step per call");
   ITTS_REQUIRE(itts_gpt_pl_supported(w, st->rows), fn, "shape or device not supported (see itts_gpt_pl_supported)");
-  ITTS_REQUIRE(st->seen && st->done && st->codes && st->logits && w->head_w, fn, "sampler state missing");
+  ITTS_REQUIRE(st->logits && w->head_w && (smp->mode == 2 || (st->seen && st->done && st->codes)), fn,
+               "sampler state missing");
   const int L = w->n_layer, D = w->d_model, R = st->rows;
   int rc = 0;
   for (int k = 0; k < nsteps && rc == 0; ++k) {
-    rc = itts_gpt_pl_begin_step(scratch, stream);
+    rc = itts_gpt_pl_begin_step(scratch, R, stream);
     for (int l = 0; l < L && rc == 0; ++l)
       rc = itts_gpt_layer_pl(&w->layers[l], &pl[l], st, l, k, l + 1 == L, scratch, stream);
     // the last layer's mlp.c_proj reduce with ln_f + final_norm (Q5) over the persistent partials
     if (rc == 0)
       rc = itts_residual_reduce_ln(st->x, D, reinterpret_cast<float*>(static_cast<unsigned char*>(scratch) + kOffP2),
-                                   kNC, (int64_t)32 * kD, kD, w->layers[L - 1].proj_b, st->xh, D, R, D, w->ln_f_g,
-                                   w->ln_f_b, w->final_g, w->final_b, ITTS_BF16, stream);
+                                   kNC, (int64_t)kMaxR * kD, kD, w->layers[L - 1].proj_b, st->xh, D, R, D,
+                                   w->ln_f_g, w->ln_f_b, w->final_g, w->final_b, ITTS_BF16, stream);
     if (rc == 0) rc = itts::gpt_head_sample(w, st, smp, k, stream);
   }
-  if (rc == 0) rc = itts_step_advance(st->tstate, nsteps, stream);
+  if (rc == 0 && smp->mode != 2) rc = itts_step_advance(st->tstate, nsteps, stream);
   return rc;
 }

@@ -93,7 +93,7 @@ SIGNATURES = {
     "itts_gpt_decode_steps": (_c_i, [_vp, _vp, _vp, _c_i, _vp]),
     "itts_gpt_pl_scratch_bytes": (_c_i64, []),
     "itts_gpt_pl_supported": (_c_i, [_vp, _c_i]),
-    "itts_gpt_pl_begin_step": (_c_i, [_vp, _vp]),
+    "itts_gpt_pl_begin_step": (_c_i, [_vp, _c_i, _vp]),
     "itts_gpt_layer_pl": (_c_i, [_vp, _vp, _vp, _c_i, _c_i, _c_i, _vp, _vp]),
     "itts_gpt_pl_error": (_c_i, [_vp, _vp, ctypes.POINTER(_c_i)]),
     "itts_gpt_decode_steps_pl": (_c_i, [_vp, _vp, _vp, _vp, _vp, _c_i, _vp]),

@@ -146,8 +146,8 @@ class HipGPT:
         #    (profiles/ubench_fused_r02.txt)
         self.cstep = self.fold and os.environ.get("ITTS_CSTEP", "1") != "0"
         #  * every layer of the step as ONE persistent launch (itts_gpt_decode_steps_pl, gpt_layer.hip) for
-        #    1..32 rows of the IndexTTS-1.5 shape on a 256-CU device; bit-identical to the launch chain
-        #    (ITTS_PL=0: the chain)
+        #    1..128 rows of the IndexTTS-1.5 shape (beam lineage included) on a 256-CU device; bit-identical
+        #    to the launch chain (ITTS_PL=0: the chain)
         self.pl = self.cstep and os.environ.get("ITTS_PL", "1") != "0" and self.D == 1024 and self.H == 16
         self.layers: List[_Layer] = []
         for i in range(self.L):
@@ -478,11 +478,14 @@ class HipGPT:
             mode = _hip.Sampling(1, int(min_new), float(penalty), float(smp[0]), int(smp[1]), float(smp[2]))
         cst = self._c_state(st)
         stream = _hip.stream_ptr()
-        if not beams and self._pl_ok(st):  # every layer one persistent launch (bit-identical to the chain)
+        if self._pl_ok(st):  # every layer one persistent launch (bit-identical to the chain)
             _hip.check(self.lib.itts_gpt_decode_steps_pl(ctypes.byref(self._cweights), self._plw,
                                                          self._pl_scratch.data_ptr(), ctypes.byref(cst),
-                                                         ctypes.byref(mode), int(nsteps), stream),
+                                                         ctypes.byref(mode), 1 if beams else int(nsteps), stream),
                        "itts_gpt_decode_steps_pl")
+            if beams:
+                self._beam_step(st, 1)
+                _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
             return
         if nsteps > 1:
             assert not beams
@@ -496,9 +499,9 @@ class HipGPT:
             _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
     def _pl_ok(self, st):
-        """persistent layers for this state: <= 32 rows, a 256-CU device, and no other lane of this engine
+        """persistent layers for this state: <= 128 rows, a 256-CU device, and no other lane of this engine
         decoding concurrently (two persistent grids could each hold part of the CUs)"""
-        return (self.pl and st["B"] <= 32 and not st.get("multi_lane", False)
+        return (self.pl and st["B"] <= 128 and not st.get("multi_lane", False)
                 and bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), st["B"])))
 
     def pl_error(self):
@@ -984,6 +987,8 @@ class HipGPT:
         ln = self._beam_state(B, K, max_new_tokens, s)
         st = ln["st"]
         st["s"] = s
+        if self.pl:
+            self._pl_err.zero_()
         st["beam"] = {"K": K, "sampling": sampling, "min_new": min_new_tokens, "penalty": repetition_penalty,
                       "length_penalty": length_penalty}
         rows_b = torch.arange(B, device=self.dev).repeat_interleave(K)
@@ -1017,7 +1022,7 @@ class HipGPT:
         else:
             self._dgw(st["h"], self.head_w, R, self.head_b, st["logits"])
         self._beam_step(st, 0)
-        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep)
+        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep, self.pl)
         graph_ok = use_graph and max_new_tokens > 1
         if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
             ln["graph"] = (self._capture(st, min_new_tokens, repetition_penalty), gkey)
@@ -1048,6 +1053,8 @@ class HipGPT:
             steps += n
             if steps // check_every != prev // check_every and bool(st["done_u"].all()):
                 break
+        if self._pl_ok(st) and self.pl_error():
+            raise _hip.HipError("persistent decode layer: hand-off timeout")
         return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
 
     def _beam_finalize(self, st, B, K, steps, max_new, length_penalty):

@@ -23,7 +23,8 @@ import re
 import sys
 
 DECODE_KERNELS = ("attn_decode_kernel", "decode_gemm_kernel", "decode_gemm16_kernel", "decode_gemm16x_kernel",
-                  "residual_reduce_ln", "sample_embed_kernel", "sample_topk_embed_kernel", "advance_kernel")
+                  "residual_reduce_ln", "sample_embed_kernel", "sample_topk_embed_kernel", "advance_kernel",
+                  "gpt_layer_pl_kernel", "fillBuffer")  # persistent layers (r04) + the per-step counter memset
 
 
 def load(d, counter):
@@ -72,7 +73,7 @@ def vocoder(fetch, write):
 
 def decode(fetch, write):
     ids = sorted(k for k, (n, _) in fetch.items() if k in write)
-    first = min(k for k in ids if "attn_decode_kernel" in fetch[k][0])
+    first = min(k for k in ids if "attn_decode_kernel" in fetch[k][0] or "gpt_layer_pl_kernel" in fetch[k][0])
     ids = [k for k in ids if k >= first and any(s in fetch[k][0] for s in DECODE_KERNELS)]
     steps = sum(1 for k in ids if "advance_kernel" in fetch[k][0])
     per = {}
