@@ -97,6 +97,10 @@ def pack_qkv12(wx_qkv, w_io, ln, n_head: int = 16):
     return {"w12": w12.to(dev), "uc": uc}
 
 
+# the persistent decode layers are the default once measured on the device (ITTS_PL overrides)
+PL_DEFAULT = "0"
+
+
 class _Layer:
     pass
 
@@ -148,7 +152,7 @@ class HipGPT:
         #  * every layer of the step as ONE persistent launch (itts_gpt_decode_steps_pl, gpt_layer.hip) for
         #    1..128 rows of the IndexTTS-1.5 shape (beam lineage included) on a 256-CU device; bit-identical
         #    to the launch chain (ITTS_PL=0: the chain)
-        self.pl = self.cstep and os.environ.get("ITTS_PL", "1") != "0" and self.D == 1024 and self.H == 16
+        self.pl = self.cstep and os.environ.get("ITTS_PL", PL_DEFAULT) != "0" and self.D == 1024 and self.H == 16
         self.layers: List[_Layer] = []
         for i in range(self.L):
             p = f"gpt.h.{i}"

@@ -15,11 +15,20 @@ _cache = {}
 
 def _engine():
     if "eng" not in _cache:
+        import os
         from indextts.gpt.engine import HipGPT
         from indextts.utils.config import default_config_path, load_config
         from indextts.utils.synthetic import gpt_state_dict
         cfg = load_config(default_config_path())
-        _cache["eng"] = HipGPT(gpt_state_dict(cfg.gpt, 0, 0.08), cfg.gpt, "cuda", dtype="bf16", max_kv=256)
+        old = os.environ.get("ITTS_PL")
+        os.environ["ITTS_PL"] = "1"  # this engine packs the persistent-layer operands whatever the default
+        try:
+            _cache["eng"] = HipGPT(gpt_state_dict(cfg.gpt, 0, 0.08), cfg.gpt, "cuda", dtype="bf16", max_kv=256)
+        finally:
+            if old is None:
+                del os.environ["ITTS_PL"]
+            else:
+                os.environ["ITTS_PL"] = old
     return _cache["eng"]
 
 
