@@ -36,7 +36,9 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 # PMC traffic summaries of the CURRENT build (profiles/run_profiles.sh; FETCH_SIZE x2 per
 # MI355X_MICROARCH.md, calibrated by profiles/pmc_calibrate.py); None when not yet measured
-TRAFFIC_DECODE = "traffic_decode_r03s.json"
+# per decoding and decode path (persistent layers or the launch chain): None until measured for this build
+TRAFFIC_DECODE = {("greedy", True): "traffic_decode_pl_r04.json", ("greedy", False): "traffic_decode_r04.json",
+                  ("beam3", True): "traffic_decode_beam3_pl_r04.json", ("beam3", False): "traffic_decode_beam3_r04.json"}
 TRAFFIC_VOCODER = "traffic_vocoder_r03s.json"
 
 
@@ -323,7 +325,7 @@ def main():
         d_bytes = sum(tts.gpt.step_weight_bytes + keys * tts.gpt.kv_bytes_per_key for _, _, _, keys in step_ev)
         gbs = d_bytes / (d_ms * 1e-3) / 1e9
         rows = step_ev[0][2]
-        pl = tts.gpt.pl and rows <= 32 and args.decoding != "beam3"
+        pl = bool(tts.gpt.pl and tts.gpt._pl_ok({"B": rows}))
         body = ("20 x ONE persistent launch per layer (gpt_layer.hip: c_attn (ln_1 folded) -> attention -> "
                 "attn.c_proj split-K 8 + reduce -> c_fc (ln_2 folded, gelu) -> mlp.c_proj split-K 8 + reduce as "
                 "phases joined by in-launch hand-offs, weights prefetched by LDS-DMA) + counter memset + "
@@ -366,8 +368,9 @@ def main():
                         "launches": n, "avg_launch_us": round(1e3 * ms / n, 2),
                         "algorithmic_bytes_per_launch": round(t.bytes / n),
                         "share_of_step": round(ms / (1e3 * dt / args.steps), 3)}
-    if dec is not None and args.decoding == "greedy":  # the decode step: the dominant unit of work
-        dec["traffic"] = _traffic(TRAFFIC_DECODE, "bytes_per_step")
+    if dec is not None:  # the decode step: the dominant unit of work
+        dec["traffic"] = _traffic(TRAFFIC_DECODE[(args.decoding, pl)], "bytes_per_step")
+        dec["traffic_source"] = f"profiles/{TRAFFIC_DECODE[(args.decoding, pl)]}"
     cpu = None
     if args.breakdown:
         ph = {}

@@ -29,6 +29,7 @@ from indextts.utils.config import default_config_path, load_config  # noqa: E402
 from indextts.utils.synthetic import gpt_state_dict  # noqa: E402
 
 B, L, STEPS = 32, 200, 96
+BEAM3 = len(sys.argv) > 1 and sys.argv[1] == "beam3"  # the reference's default decoding: 3 beams x 32
 
 
 def main():
@@ -38,10 +39,14 @@ def main():
     g = np.random.default_rng(2)
     conds = torch.from_numpy(g.normal(0, 1, (B, 32, eng.D)).astype(np.float32)).cuda()
     text = torch.from_numpy(g.integers(2, 12000, (B, L))).cuda()
-    codes = eng.generate(conds, text, STEPS, min_new_tokens=STEPS, use_graph=False, check_every=10 ** 9)
+    if BEAM3:
+        codes = eng.generate(conds, text, STEPS, min_new_tokens=STEPS, use_graph=False, check_every=10 ** 9,
+                             num_beams=3, do_sample=True, top_k=30, top_p=0.8, seed=1234)
+    else:
+        codes = eng.generate(conds, text, STEPS, min_new_tokens=STEPS, use_graph=False, check_every=10 ** 9)
     torch.cuda.synchronize()
     s = 32 + L + 2
-    print(f"decode steps: {STEPS - 1} (after prefill), codes {tuple(codes.shape)}, "
+    print(f"decode steps: {STEPS - 1} (after prefill), beam3 {BEAM3}, persistent layers {eng.pl}, codes {tuple(codes.shape)}, "
           f"mean keys per row {s + 2 + (STEPS - 2) / 2:.1f} (= bench.py C3)")
 
 
