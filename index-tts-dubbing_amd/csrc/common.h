@@ -93,6 +93,26 @@ __device__ __forceinline__ float sum8_dpp(float v) {
   return v;
 }
 
+// ---- the folded-LayerNorm GEMM epilogue (itts_decode_gemm16x and the persistent layer, gpt_layer.hip):
+// one fixed rounding sequence with FMA contraction off, so the two kernels agree bit for bit whatever
+// the compiler would fuse in each context (round 4: a contracted rs * t + c in one of them and not in
+// the other left q/k/v 1 ulp apart) ----
+__device__ __forceinline__ void fold_mu_rs(float S, float Q, float inv, float eps, float& mu, float& rs) {
+#pragma clang fp contract(off)
+  const float m = S * inv;
+  mu = m;
+  rs = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + eps);
+}
+__device__ __forceinline__ float fold_apply(float acc, float rs, float mu, float u, float c) {
+#pragma clang fp contract(off)
+  return rs * (acc - mu * u) + c;
+}
+__device__ __forceinline__ float gelu_tanh_nc(float x) {
+#pragma clang fp contract(off)
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
 // ---- host-side error plumbing (no C++ exception crosses the C ABI) ----
 namespace itts {
 void set_error(const std::string& msg);

@@ -455,9 +455,7 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
         S += rsum[ww][r];
         Q += rsq[ww][r];
       }
-      const float inv = 1.0f / p.K, m = S * inv;
-      mu[r] = m;
-      rs[r] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
+      fold_mu_rs(S, Q, 1.0f / p.K, p.eps, mu[r], rs[r]);
     }
     __syncthreads();
   }
@@ -479,15 +477,15 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
       const int row = 32 * tile + 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
       const int n = nt * 16 + (l & 15);
       if (row >= p.M || n >= p.N) continue;
-      if constexpr (FOLD) v = rs[row] * (v - mu[row] * p.u[n]);
-      if (p.c) v += p.c[n];
+      if constexpr (FOLD) v = fold_apply(v, rs[row], mu[row], p.u[n], p.c ? p.c[n] : 0.f);
+      else if (p.c) v += p.c[n];
       if constexpr (EPI == 1) {
         float* X = reinterpret_cast<float*>(p.y) + (int64_t)row * p.ldy + n;
         const float xv = *X + v;
         st_out(X, xv);
         st_out(p.xh + (int64_t)row * p.ldxh + n, f2bf(xv));
       } else {
-        if (p.gelu) v = gelu_tanh_d(v);
+        if (p.gelu) v = gelu_tanh_nc(v);
         St<OutT>::st(reinterpret_cast<OutT*>(p.y) + (int64_t)row * p.ldy + n, v);
       }
     }

@@ -98,11 +98,6 @@ struct PlArgs {
   unsigned char* scratch;
 };
 
-__device__ __forceinline__ float gelu_tanh_pl(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
-}
-
 // workgroup barrier that waits for this wave's LDS traffic only: a __syncthreads() would also drain
 // every vector-memory load in flight (the K/V rows requested ahead of the c_attn phase)
 __device__ __forceinline__ void bar() {
@@ -265,9 +260,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         S += rsum[ww * 32 + tid];
         Q += rsq[ww * 32 + tid];
       }
-      const float inv = 1.0f / kD, m = S * inv;
-      mu[tid] = m;
-      rsd[tid] = rsqrtf(fmaxf(Q * inv - m * m, 0.f) + p.eps);
+      fold_mu_rs(S, Q, 1.0f / kD, p.eps, mu[tid], rsd[tid]);
     }
   };
 
@@ -316,8 +309,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
         const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = 32 * t + rt;
         const float* uc = p.qkv_uc + (int64_t)b * 2 * kQC;
-        v = rsd[rt] * (v - mu[rt] * uc[col]);
-        v += uc[kQC + col];
+        v = fold_apply(v, rsd[rt], mu[rt], uc[col], uc[kQC + col]);
         const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
         const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
         __hip_atomic_store(gq + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -610,9 +602,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
         const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
         const int n = (32 * c + j) * 16 + (l & 15);
-        v = rsd[rt] * (v - mu[rt] * p.fc_u[n]);
-        v += p.fc_c[n];
-        v = gelu_tanh_pl(v);
+        v = gelu_tanh_nc(fold_apply(v, rsd[rt], mu[rt], p.fc_u[n], p.fc_c[n]));
         obf[rt * 16 + (l & 15)] = f2bf(v);
       }
       bar();
