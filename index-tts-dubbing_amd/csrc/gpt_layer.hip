@@ -50,18 +50,41 @@ constexpr int kQC = 12;                               // c_attn columns per work
 constexpr int kKB = 8;                                // attention keys per group per round (load depth)
 constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
 constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s), then the grid drains
+// ITTS_PL_TRACE=1 (timing builds): wave 0 of every workgroup stamps the 100-MHz real-time counter at
+// the phase boundaries of layer ITTS_PL_TRACE_LAYER into the scratch trace block (profiles/pl_trace.py)
+#ifndef ITTS_PL_TRACE
+#define ITTS_PL_TRACE 0
+#endif
+#ifndef ITTS_PL_TRACE_LAYER
+#define ITTS_PL_TRACE_LAYER 10
+#endif
+// ITTS_PL_DMA_EARLY=1: the later phases' weight DMA is issued at launch start, ahead of the c_attn
+// operands' arrival (round-4 first version); default: right after the c_attn MFMAs, so the burst does
+// not queue in front of the critical-path loads (profiles/pl_trace_r04*.txt)
+#ifndef ITTS_PL_DMA_EARLY
+#define ITTS_PL_DMA_EARLY 0
+#endif
 
 // scratch layout (bytes) for up to kMaxR rows; the counters and the granules of the step's rows are zeroed
 // before every step
 constexpr int kMaxR = 128;
+// hand-off counters, one per 4-KiB block: 256 workgroups polling counters that share one line saturated
+// it (hand-offs observed 2.5-6 us after the last arrival, profiles/pl_trace_r04b.txt); ITTS_PL_CNT_STRIDE=1
+// packs them (A/B)
+#ifndef ITTS_PL_CNT_STRIDE
+#define ITTS_PL_CNT_STRIDE 1024
+#endif
+constexpr int kCntStride = ITTS_PL_CNT_STRIDE;  // u32 units
+constexpr int kNumCnt = 88;
 constexpr int64_t kOffCnt = 0;
-constexpr int64_t kOffGq = 512;                                       // [128 rows][16 heads][192] u64
+constexpr int64_t kOffGq = ((int64_t)kNumCnt * kCntStride * 4 + 511) / 512 * 512;                                       // [128 rows][16 heads][192] u64
 constexpr int64_t kOffOb = kOffGq + (int64_t)kMaxR * kH * 192 * 8;    // [8][128][128] bf16
 constexpr int64_t kOffP1 = kOffOb + (int64_t)kNC * kMaxR * 128 * 2;   // [8][128][1024] f32
 constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * kMaxR * kD * 4;    // [8][128][1024] bf16
 constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * kMaxR * kD * 2;    // [8][128][512] bf16
 constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * kMaxR * 512 * 2;   // [8][128][1024] f32
-constexpr int64_t kOffErr = kOffP2 + (int64_t)kNC * kMaxR * kD * 4;   // sticky error word (not zeroed per step)
+constexpr int64_t kOffTrace = kOffP2 + (int64_t)kNC * kMaxR * kD * 4; // [256 WG][32] u64 (ITTS_PL_TRACE builds)
+constexpr int64_t kOffErr = kOffTrace + (int64_t)kWG * 32 * 8;        // sticky error word (not zeroed per step)
 constexpr int64_t kScratchBytes = kOffErr + 256;
 inline int64_t zero_bytes(int rows) { return kOffGq + (int64_t)rows * kH * 192 * 8; }  // multiple of 16
 enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56 };
@@ -162,6 +185,12 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   uint16_t* obf = reinterpret_cast<uint16_t*>(smem + L_OBF);  // o staging [2][64], then f tiles [32][16]
   const int R = p.R;
   if (tid == 0) *abort_flag = 0;
+  uint64_t* trace = reinterpret_cast<uint64_t*>(p.scratch + kOffTrace) + 32 * b;
+  const bool tr = ITTS_PL_TRACE && p.layer == ITTS_PL_TRACE_LAYER && tid == 0;
+  auto mark = [&](int i) {
+    if (tr) trace[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  mark(0);
 
   const int w = wave;
   const int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
@@ -191,33 +220,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   // ---- (A0) c_attn operands first (weights nt, 12 of 16 fragment columns real; A = x^ tile 0), then the
   // attention's first round of K/V rows (pass 0), then the residual slices, then the weight DMA
   u32x4_t bw[4], av[4][2];
-  float2 x_old[MT];
-  {
-    const u32x4_t* wq = p.qkv_w12 + (int64_t)b * 32 * 4 * kQC;
+  float2 x_raw[MT];  // the residual slices, issued first (selected at phase D: no early wait on them)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int s = w + 8 * i;
-      bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    {
-      const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
-      const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
-      kv_load(kr, p.kc, rr, p0, nk, 0);
-      kv_load(vr, p.vc, rr, p0, nk, 0);
-    }
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const int row = 32 * t + xrow, xr = row < R ? row : R - 1;
-      const float2 xv = *reinterpret_cast<const float2*>(p.x + (int64_t)xr * kD + xcol);
-      x_old[t] = row < R ? xv : float2{0.f, 0.f};
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // this workgroup's attn.c_proj (8 KiB), c_fc (32 KiB), mlp.c_proj (32 KiB) weight slices, global ->
-    // LDS by DMA (1 KiB per wave instruction, lane-linear = fragment order, nt), instruction t by wave t % 8
+  for (int t = 0; t < MT; ++t) {
+    const int row = 32 * t + xrow, xr = row < R ? row : R - 1;
+    x_raw[t] = *reinterpret_cast<const float2*>(p.x + (int64_t)xr * kD + xcol);
+  }
+  // this workgroup's attn.c_proj (8 KiB), c_fc (32 KiB), mlp.c_proj (32 KiB) weight slices, global ->
+  // LDS by DMA (1 KiB per wave instruction, lane-linear = fragment order, nt), instruction t by wave t % 8
+  auto issue_dma = [&]() {
 #pragma unroll
     for (int m = 0; m < 9; ++m) {
       const int t = w + 8 * m;
@@ -235,7 +246,30 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       }
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(smem + dst), 16, 0, 2);
     }
+  };
+  {
+    const u32x4_t* wq = p.qkv_w12 + (int64_t)b * 32 * 4 * kQC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = w + 8 * i;
+      bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
+      const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+      kv_load(kr, p.kc, rr, p0, nk, 0);
+      kv_load(vr, p.vc, rr, p0, nk, 0);
+    }
+    if (ITTS_PL_DMA_EARLY) {
+      __builtin_amdgcn_sched_barrier(0);
+      issue_dma();
+    }
   }
+  mark(1);
 
   // fold statistics of one 32-row tile (the A fragments a wave accumulated): sums -> mu / rstd in LDS
   auto fold_stats = [&](const float (&ss)[2], const float (&sq)[2]) {
@@ -322,6 +356,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
     if (MT > 1) bar();  // red / statistics are reused by the next tile
   }
+  mark(2);
 
   // ---- (E1 + B) attention passes: unit u of pass pt = row 32 pt + 2 jj + u of head h (attn_decode_kernel
   // algorithm: 32 groups x 8 lanes, keys g + 32 n, fixed kSub-key softmax chunks, fixed-order merge)
@@ -374,7 +409,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       }
     }
     bar();
+    if (pt == 0) mark(3);
     if (*abort_flag) return;
+    // the later phases' weights: behind the c_attn operands and this pass's K/V rows, after the q/k/v
+    // granule sweep (a burst issued earlier queued in front of those loads: profiles/pl_trace_r04b.txt)
+    if (!ITTS_PL_DMA_EARLY && pt == 0) issue_dma();
     if (act_u) {
       float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       float m_run = -INFINITY, l_run = 0.f;
@@ -485,12 +524,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
     if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
+  mark(4);
   drain();  // the o stores, and this wave's weight DMA (read from LDS from phase C on)
   bar();
-  if (tid == 0) add_relaxed(cnt + CNT2 + c);
+  mark(15);
+  if (tid == 0) add_relaxed(cnt + (CNT2 + c) * kCntStride);
 
   // ---- (C) attn.c_proj split c, tile j, per 32-row tile: decode_gemm_kernel EPI 2 (one k-step per wave)
-  if (tid == 0 && !poll_ge(cnt + CNT2 + c, kCPC * L1, err, 2)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt + (CNT2 + c) * kCntStride, kCPC * L1, err, 2)) *abort_flag = 1;
+  mark(5);
   bar();
   if (*abort_flag) return;
   auto store_partial = [&](float* dst, int t) {  // 1024 outputs of row tile t, 2 per thread, fixed-order sum
@@ -524,12 +566,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       bar();
     }
   }
+  mark(6);
   drain();
   bar();
-  if (tid == 0) add_relaxed(cnt + CNT3 + j);
+  mark(16);
+  if (tid == 0) add_relaxed(cnt + (CNT3 + j) * kCntStride);
 
   // ---- (D) x1 = x + (b_o + sum_c partial_c) on tile j (residual_reduce_ln_v4 order), x1^ -> cluster copy
-  if (tid == 0 && !poll_ge(cnt + CNT3 + j, kNC * L1, err, 3)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt + (CNT3 + j) * kCntStride, kNC * L1, err, 3)) *abort_flag = 1;
+  mark(7);
   bar();
   if (*abort_flag) return;
   float2 x1[MT];
@@ -545,17 +590,21 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         pp.x += __uint_as_float((uint32_t)v);
         pp.y += __uint_as_float((uint32_t)(v >> 32));
       }
-      x1[t] = float2{x_old[t].x + pp.x, x_old[t].y + pp.y};
+      const float2 xo = row < R ? x_raw[t] : float2{0.f, 0.f};
+      x1[t] = float2{xo.x + pp.x, xo.y + pp.y};
       st_sc1_u32(reinterpret_cast<uint32_t*>(xc + (((int64_t)c * kMaxR + row) * kD + xcol) * 2),
                  pack2bf(x1[t].x, x1[t].y));
     }
   }
+  mark(8);
   drain();
   bar();
-  if (tid == 0) add_relaxed(cnt + CNT4 + c);
+  mark(17);
+  if (tid == 0) add_relaxed(cnt + (CNT4 + c) * kCntStride);
 
   // ---- (E) c_fc (ln_2 folded) + gelu on column tile 32c + j, per row tile, A = the cluster's x1^
-  if (tid == 0 && !poll_ge(cnt + CNT4 + c, kCPC * L1, err, 4)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt + (CNT4 + c) * kCntStride, kCPC * L1, err, 4)) *abort_flag = 1;
+  mark(9);
   bar();
   if (*abort_flag) return;
   {
@@ -615,12 +664,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       if (MT > 1) bar();
     }
   }
+  mark(10);
   drain();
   bar();
-  if (tid == 0) add_relaxed(cnt + CNT5 + c);
+  mark(18);
+  if (tid == 0) add_relaxed(cnt + (CNT5 + c) * kCntStride);
 
   // ---- (F) mlp.c_proj split c, tile j, per row tile: decode_gemm_kernel EPI 2 (k-steps w + 8i of the split)
-  if (tid == 0 && !poll_ge(cnt + CNT5 + c, kCPC * L1, err, 5)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt + (CNT5 + c) * kCntStride, kCPC * L1, err, 5)) *abort_flag = 1;
+  mark(11);
   bar();
   if (*abort_flag) return;
   {
@@ -647,9 +699,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       bar();
     }
   }
+  mark(12);
   drain();
   bar();
-  if (tid == 0) add_relaxed(cnt + CNT6 + j);
+  mark(19);
+  if (tid == 0) add_relaxed(cnt + (CNT6 + j) * kCntStride);
 
   // ---- (G) x2 = x1 + (b_proj + sum_c partial_c); x, x^ for the next launch (cluster c: rows 4c .. 4c+3 of
   // every tile).  The last layer stores x1 and leaves this reduce (with ln_f + final_norm, Q5) to
@@ -662,7 +716,8 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
     return;
   }
-  if (tid == 0 && !poll_ge(cnt + CNT6 + j, kNC * L1, err, 6)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt + (CNT6 + j) * kCntStride, kNC * L1, err, 6)) *abort_flag = 1;
+  mark(13);
   bar();
   if (*abort_flag) return;
   if ((xrow >> 2) == c) {
@@ -683,6 +738,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       *reinterpret_cast<uint32_t*>(p.xh + (int64_t)row * kD + xcol) = pack2bf(x2.x, x2.y);
     }
   }
+  mark(14);
 }
 
 int g_cu_count = -1;

@@ -17,6 +17,8 @@
 // the Infinity Cache on a side stream: attention with cache-resident K/V is 9.7 vs 12.7 us, but the
 // side stream slowed the whole step from 830 to 1327 us; each kernel requesting a later kernel's
 // weights into the Infinity Cache in-kernel (profiles/prefetch_ab_r02.txt): every plan slower.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -38,6 +40,15 @@ extern "C" int itts_gpt_decode_state_bytes(const ItTsGptWeights* w, int rows, in
 }
 
 namespace {
+// ITTS_OPROJ_EPI=1: attn.c_proj as one 16-column launch with the residual epilogue (round 3) instead of
+// split-K 8 + reduce (the persistent layer's arithmetic)
+bool oproj_epi() {
+  static const bool on = [] {
+    const char* e = getenv("ITTS_OPROJ_EPI");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 // one decode step without the step-counter advance; step k of a multi-step call reads key
 // kv_base + tstate[0] + k and writes code column tstate[0] + 1 + k (so ONE advance by n follows n
 // steps: the advance kernel is a whole dependent launch per step otherwise)
@@ -77,12 +88,18 @@ int decode_step_impl(const ItTsGptWeights* w, const ItTsGptDecodeState* st, cons
     // attn.c_proj: split-K 8 partials (one per head pair), then x += b_o + sum, x^ = bf16(x) -- the
     // persistent layer's arithmetic (gpt_layer.hip: each cluster of 32 CUs owns two heads), so both
     // paths give the same bits (round 3: one 16-column residual-epilogue launch, 5.4 us)
-    if (rc == 0)
-      rc = itts_decode_gemm(st->o, D, ly.o_w, D, D, R, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 2, st->part,
-                            D, ITTS_F32, (int64_t)R * D, kMlpSplit, stream);
-    if (rc == 0)
-      rc = itts_residual_reduce_ln(st->x, D, st->part, kMlpSplit, (int64_t)R * D, D, ly.o_c, st->xh, D, R, D, nullptr,
-                                   nullptr, nullptr, nullptr, ITTS_BF16, stream);
+    if (oproj_epi()) {  // one 16-column launch with the residual epilogue (A/B)
+      if (rc == 0)
+        rc = itts_decode_gemm16x(st->o, D, ly.o_w16, D, D, R, ly.o_c, nullptr, eps, 0, 1, st->x, D, ITTS_F32, st->xh, D,
+                                 8, stream);
+    } else {
+      if (rc == 0)
+        rc = itts_decode_gemm(st->o, D, ly.o_w, D, D, R, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 2, st->part,
+                              D, ITTS_F32, (int64_t)R * D, kMlpSplit, stream);
+      if (rc == 0)
+        rc = itts_residual_reduce_ln(st->x, D, st->part, kMlpSplit, (int64_t)R * D, D, ly.o_c, st->xh, D, R, D, nullptr,
+                                     nullptr, nullptr, nullptr, ITTS_BF16, stream);
+    }
     // ln_2 (folded) + c_fc + gelu -> f bf16
     if (rc == 0)
       rc = itts_decode_gemm16x(st->xh, D, ly.fc_w16, D, 4 * D, R, ly.fc_c, ly.fc_u, eps, 1, 0, st->f, 4 * D, ITTS_BF16,

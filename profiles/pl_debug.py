@@ -16,7 +16,18 @@ from indextts.gpt.engine import HipGPT  # noqa: E402
 from indextts.utils.config import default_config_path, load_config  # noqa: E402
 from indextts.utils.synthetic import gpt_state_dict  # noqa: E402
 
-OFF_GQ, OFF_OB, OFF_P1, OFF_XC, OFF_FC, OFF_P2 = 512, 3146240, 3408384, 7602688, 9699840, 10748416
+
+
+def offsets(nbytes):
+    """scratch regions of gpt_layer.hip, counted back from its end: err 256 B, trace 64 KiB, then P2, FC,
+    XC, P1, OB, GQ (their sizes are fixed by the 128-row capacity)"""
+    p2 = nbytes - 256 - 256 * 32 * 8 - 8 * 128 * 1024 * 4
+    fc = p2 - 8 * 128 * 512 * 2
+    xc = fc - 8 * 128 * 1024 * 2
+    p1 = xc - 8 * 128 * 1024 * 4
+    ob = p1 - 8 * 128 * 128 * 2
+    gq = ob - 128 * 16 * 192 * 8
+    return gq, ob, p1, xc, fc, p2
 
 
 def cmp(name, a, b):
@@ -65,6 +76,7 @@ def main(B):
     torch.cuda.synchronize()
     print(f"  pl_error={eng.pl_error()}", flush=True)
     sc = eng._pl_scratch.view(torch.uint8)
+    OFF_GQ, OFF_OB, OFF_P1, OFF_XC, OFF_FC, OFF_P2 = offsets(int(lib.itts_gpt_pl_scratch_bytes()))
     gq = sc[OFF_GQ:OFF_GQ + 128 * 16 * 192 * 8].view(torch.int64).view(128, 16, 192)[:B]
     gval = (gq & 0xFFFFFFFF).to(torch.int32).view(torch.float32)
     gtag = (gq >> 32)

@@ -32,7 +32,21 @@ B, L, STEPS = 32, 200, 96
 BEAM3 = len(sys.argv) > 1 and sys.argv[1] == "beam3"  # the reference's default decoding: 3 beams x 32
 
 
+def _heartbeat():
+    """a line every 30 s: counter passes over the 96-row beam step run for minutes without output"""
+    import threading
+    import time
+
+    def beat():
+        t0 = time.time()
+        while True:
+            time.sleep(30)
+            print(f"[pmc_decode] running {time.time() - t0:.0f} s", flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
+    _heartbeat()
     cfg = load_config(default_config_path())
     eng = HipGPT(gpt_state_dict(cfg.gpt, seed=0, mel_head_std=0.08), cfg.gpt, "cuda", "bf16",
                  max_kv=32 + L + 2 + 1 + STEPS + 8)
