@@ -61,6 +61,9 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 // ITTS_PL_DMA_EARLY=1: the later phases' weight DMA is issued at launch start, ahead of the c_attn
 // operands' arrival (round-4 first version); default: right after the c_attn MFMAs, so the burst does
 // not queue in front of the critical-path loads (profiles/pl_trace_r04*.txt)
+#ifndef ITTS_PL_DBG
+#define ITTS_PL_DBG 0
+#endif
 #ifndef ITTS_PL_DMA_EARLY
 #define ITTS_PL_DMA_EARLY 0
 #endif
@@ -191,6 +194,12 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     if (tr) trace[i] = __builtin_amdgcn_s_memrealtime();
   };
   mark(0);
+  // ITTS_PL_DBG (debug builds): layer 0 of a generate's first decode step stores what wave 0 read into
+  // trace slots 20..31 (profiles/lf_dbg.py)
+  const bool dbg_on = ITTS_PL_DBG && p.layer == 0 && p.tstate[0] + p.kstep == 0 && tid == 0;
+  auto dbg = [&](int i, uint32_t v) {
+    if (dbg_on) trace[20 + i] = v;
+  };
 
   const int w = wave;
   const int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
@@ -270,6 +279,13 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
   }
   mark(1);
+  dbg(0, (uint32_t)kidx);
+  dbg(1, (uint32_t)(p.pad ? p.pad[0] : 0));
+  dbg(2, av[0][0][0]);
+  dbg(3, __float_as_uint(x_raw[0].x));
+  dbg(4, bw[0][0]);
+  dbg(5, kr[0][0]);
+  dbg(6, vr[0][0]);
 
   // fold statistics of one 32-row tile (the A fragments a wave accumulated): sums -> mu / rstd in LDS
   auto fold_stats = [&](const float (&ss)[2], const float (&sq)[2]) {
@@ -410,6 +426,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
     bar();
     if (pt == 0) mark(3);
+    if (pt == 0) {
+      dbg(7, __float_as_uint(qs[0]));
+      dbg(8, __float_as_uint(kn[0]));
+      dbg(9, __float_as_uint(vn[0]));
+    }
     if (*abort_flag) return;
     // the later phases' weights: behind the c_attn operands and this pass's K/V rows, after the q/k/v
     // granule sweep (a burst issued earlier queued in front of those loads: profiles/pl_trace_r04b.txt)
@@ -525,6 +546,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
   mark(4);
+  dbg(10, obf[0]);
   drain();  // the o stores, and this wave's weight DMA (read from LDS from phase C on)
   bar();
   mark(15);

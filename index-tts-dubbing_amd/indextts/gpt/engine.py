@@ -97,9 +97,11 @@ def pack_qkv12(wx_qkv, w_io, ln, n_head: int = 16):
     return {"w12": w12.to(dev), "uc": uc}
 
 
-# the persistent decode layers are the default (measured faster: C3 decode step 710 vs 765 us,
-# profiles/pl_trace_r04c.txt); ITTS_PL=0 selects the launch chain
-PL_DEFAULT = "1"
+# the persistent decode layers (ITTS_PL=1) are faster (C3 decode step 710 vs 765 us,
+# profiles/pl_trace_r04c.txt) but OFF by default: on a decode lane reused across infer() calls the first
+# step after the prefill can read wrong data (tests/test_gpu_longform.py, profiles/lf_bisect*.py) --
+# under investigation
+PL_DEFAULT = "0"
 
 
 class _Layer:
