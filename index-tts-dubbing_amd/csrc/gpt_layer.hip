@@ -64,6 +64,21 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 #ifndef ITTS_PL_DBG
 #define ITTS_PL_DBG 0
 #endif
+// A/B switches for the hand-off memory protocol: ITTS_PL_SYS=1 makes every hand-off access system scope
+// (sc0 sc1), ITTS_PL_ACQ=1 adds an agent-scope acquire after every matched poll / granule sweep
+#ifndef ITTS_PL_SYS
+#define ITTS_PL_SYS 0
+#endif
+#ifndef ITTS_PL_ACQ
+#define ITTS_PL_ACQ 0
+#endif
+#if ITTS_PL_SYS
+#define PL_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
+#define PL_AUX 17
+#else
+#define PL_SCOPE __HIP_MEMORY_SCOPE_AGENT
+#define PL_AUX 16
+#endif
 #ifndef ITTS_PL_DMA_EARLY
 #define ITTS_PL_DMA_EARLY 0
 #endif
@@ -135,25 +150,31 @@ __device__ __forceinline__ void bar() {
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, PL_SCOPE);
 }
 __device__ __forceinline__ void add_relaxed(uint32_t* p) {
-  __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, PL_SCOPE);
 }
 __device__ __forceinline__ void st_sc1_u32(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, PL_SCOPE);
 }
 __device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, PL_SCOPE);
 }
 
 // one lane polls `ctr` until >= target (bounded); returns false on timeout / a failed grid
 __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uint32_t code) {
   for (uint32_t n = 0;; ++n) {
-    if (ld_relaxed(ctr) >= target) return true;
+    if (ld_relaxed(ctr) >= target) {
+      if (ITTS_PL_ACQ) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      return true;
+    }
     if ((n & 255) == 255 && ld_relaxed(err) != 0) return false;
     if (n > kSpinMax) {
-      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, PL_SCOPE);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -362,7 +383,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         v = fold_apply(v, rsd[rt], mu[rt], uc[col], uc[kQC + col]);
         const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
         const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
-        __hip_atomic_store(gq + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gq + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, PL_SCOPE);
         if (i >= kHD && row < R) {  // this step's key / value into the row's own cache row (0 + v, rounded)
           uint16_t* dst = (i < 2 * kHD ? p.kc : p.vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
                           (int64_t)kidx * kHD + (i & (kHD - 1));
@@ -408,6 +429,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         const bool mine = (uint32_t)(g0 >> 32) == L1 && (uint32_t)(g1 >> 32) == L1 && (uint32_t)(g2 >> 32) == L1;
         if (__all(mine)) {
           ok = true;
+          if (ITTS_PL_ACQ) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           break;
         }
         if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err) != 0)) break;
@@ -415,7 +440,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       }
       if (!ok) {
         if (lane == 0) {
-          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, PL_SCOPE);
           *abort_flag = 1;
         }
       } else {
@@ -541,7 +566,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     if (tu < 8) {  // o rows -> the cluster's [rows][128] tile, write-through 16-B stores
       const int d0 = 8 * tu;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
-      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_ob, ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_ob, ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, PL_AUX);
     }
     if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
@@ -575,7 +600,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll 1
     for (int t = 0; t < MT; ++t) {
       const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(
-          rsrc_ob, ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, 16);
+          rsrc_ob, ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, PL_AUX);
       f32x16_t acc32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
@@ -640,7 +665,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
           ax[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
-              rsrc, ((c * kMaxR + 32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, 16);
+              rsrc, ((c * kMaxR + 32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
       f32x4_t af[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
       float fs[2] = {0.f, 0.f}, fq[2] = {0.f, 0.f};
 #pragma unroll
@@ -681,7 +706,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         const int rt = tid >> 1, half = tid & 1;
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + rt * 16 + 8 * half);
         __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_f, ((c * kMaxR + 32 * t + rt) * 512 + 16 * j + 8 * half) * 2,
-                                               0, 16);
+                                               0, PL_AUX);
       }
       if (MT > 1) bar();
     }
@@ -705,7 +730,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         a4[i] = __builtin_amdgcn_raw_buffer_load_b128(
-            rsrc, ((c * kMaxR + 32 * t + r32) * 512 + 16 * (w + 8 * i) + 8 * hb) * 2, 0, 16);
+            rsrc, ((c * kMaxR + 32 * t + r32) * 512 + 16 * (w + 8 * i) + 8 * hb) * 2, 0, PL_AUX);
       f32x16_t acc32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc32[r] = 0.f;

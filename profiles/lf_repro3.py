@@ -8,6 +8,7 @@ import tempfile
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+os.environ.setdefault("ITTS_PL", "1")  # build the persistent-layer operands (opt-in path)
 sys.path.insert(0, os.path.join(HERE, "..", "index-tts-dubbing_amd"))
 sys.path.insert(0, os.path.join(HERE, "..", "tests"))
 from test_gpu_longform import CUES, GREEDY, _write_prompt  # noqa: E402

@@ -246,8 +246,10 @@ def test_vocoder_matches_reference_golden(golden, tag):
     got = wav.cpu().numpy()
     rel = np.sqrt(np.mean((got - ref) ** 2) / np.mean(ref ** 2))
     record(f"vocoder_golden_{tag}", rel_rms=rel, max_abs=float(np.abs(got - ref).max()))
-    assert rel <= 2e-2, rel
-    assert np.abs(got - ref).max() <= 0.05
+    # <= 1.5x the round-4 measurement (profiles/parity_r04d.json: tiny 8.4e-3 / 9.7e-3, full 1.01e-2 / 7.9e-3)
+    bar_rel, bar_max = {"tiny": (1.3e-2, 0.015), "full": (1.55e-2, 0.012)}[tag]
+    assert rel <= bar_rel, rel
+    assert np.abs(got - ref).max() <= bar_max
     # int16: exactly the Q8 conversion of the kernel's own waveform; vs the reference's int16 at most
     # the scaled float error + 1 (was a flat 0.05 * 32767 LSB bound)
     check_pcm(got[0], pcm[0].cpu().numpy(), ref[0], golden[f"{tag}_bv_int16"][0, 0])
@@ -256,8 +258,8 @@ def test_vocoder_matches_reference_golden(golden, tag):
 # stage-local bar: each stage's output vs the fp32 oracle stage fed the SAME bf16 stage input, so only
 # that stage's own arithmetic (bf16 storage of its ~20 intermediate tensors, MFMA accumulation) is
 # compared; an indexing / edge error inside one stage cannot hide under the end-to-end 2e-2 bar.
-STAGE_REL = 6e-3     # measured r04: see profiles/parity_r04.json "vocoder_stage*"
-EDGE_REL = 1.2e-2    # the first / last 64 output rows of every utterance (edge padding paths)
+STAGE_REL = 5.5e-3   # measured r04 <= 3.6e-3: profiles/parity_r04d.json "vocoder_stage*" (1.5x)
+EDGE_REL = 5.5e-3    # the first / last 64 output rows of every utterance (edge padding paths; measured <= 3.6e-3)
 
 
 def test_vocoder_stage_local_parity():
