@@ -888,9 +888,28 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
 }
 
 // zero the step's counters and the granules of its rows (one memset node ahead of the layer launches)
+// ITTS_PL_ZERO_KERNEL=1 (default): the step's counters / granules are zeroed by this kernel, an ordinary
+// kernel node in a captured graph (=0: hipMemsetAsync, a memset node, kept as the A/B form)
+#ifndef ITTS_PL_ZERO_KERNEL
+#define ITTS_PL_ZERO_KERNEL 1
+#endif
+namespace {
+__global__ __launch_bounds__(256) void pl_zero_kernel(u32x4_t* p, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256)
+    p[i] = u32x4_t{0u, 0u, 0u, 0u};
+}
+}  // namespace
+
 extern "C" int itts_gpt_pl_begin_step(void* scratch, int rows, void* stream) {
   const char* fn = "itts_gpt_pl_begin_step";
   ITTS_REQUIRE(scratch && rows >= 1 && rows <= kMaxR, fn, "null scratch or rows outside 1..128");
+  const int64_t n16 = zero_bytes(rows) / 16;
+  if (ITTS_PL_ZERO_KERNEL) {
+    const int blocks = (int)((n16 + 255) / 256 < 1024 ? (n16 + 255) / 256 : 1024);
+    hipLaunchKernelGGL(pl_zero_kernel, dim3(blocks), dim3(256), 0, itts::as_stream(stream),
+                       static_cast<u32x4_t*>(scratch), n16);
+    return itts::check_launch(fn);
+  }
   if (hipMemsetAsync(scratch, 0, zero_bytes(rows), itts::as_stream(stream)) != hipSuccess) return itts::check_launch(fn);
   return 0;
 }

@@ -97,11 +97,11 @@ def pack_qkv12(wx_qkv, w_io, ln, n_head: int = 16):
     return {"w12": w12.to(dev), "uc": uc}
 
 
-# the persistent decode layers (ITTS_PL=1) are faster (C3 decode step 710 vs 765 us,
-# profiles/pl_trace_r04c.txt) but OFF by default: on a decode lane reused across infer() calls the first
-# step after the prefill can read wrong data (tests/test_gpu_longform.py, profiles/lf_bisect*.py) --
-# under investigation
-PL_DEFAULT = "0"
+# the persistent decode layers are the default (C3 decode step 710 vs 765 us on the launch chain,
+# profiles/pl_trace_r04c.txt); ITTS_PL=0 selects the chain.  Their per-step counter / granule reset is a
+# kernel: as a hipMemsetAsync node it let 30 of 64 reused-lane cues decode wrong data
+# (profiles/lf_stress_memset.txt vs lf_stress_default.txt)
+PL_DEFAULT = "1"
 
 
 class _Layer:
@@ -505,10 +505,15 @@ class HipGPT:
             self._beam_step(st, 1)
             _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
+    # rows up to which a step runs on the persistent layers: one 32-row tile (C3 705.9 vs 761 us per step,
+    # C2 599 vs 613); at 96 rows (beam3) the launch chain is faster (1384 vs 1609 us, bench_r04e_b3.json
+    # vs bench_r04a_b3_pl0.json), so beams and the 128-row long-form chunks stay on the chain
+    PL_MAX_ROWS = int(os.environ.get("ITTS_PL_MAX_ROWS", "32"))
+
     def _pl_ok(self, st):
-        """persistent layers for this state: <= 128 rows, a 256-CU device, and no other lane of this engine
-        decoding concurrently (two persistent grids could each hold part of the CUs)"""
-        return (self.pl and st["B"] <= 128 and not st.get("multi_lane", False)
+        """persistent layers for this state: <= PL_MAX_ROWS (<= 128) rows, a 256-CU device, and no other
+        lane of this engine decoding concurrently (two persistent grids could each hold part of the CUs)"""
+        return (self.pl and st["B"] <= min(self.PL_MAX_ROWS, 128) and not st.get("multi_lane", False)
                 and bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), st["B"])))
 
     def pl_error(self):

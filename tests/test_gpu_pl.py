@@ -24,6 +24,7 @@ def _engine():
         os.environ["ITTS_PL"] = "1"  # this engine packs the persistent-layer operands whatever the default
         try:
             _cache["eng"] = HipGPT(gpt_state_dict(cfg.gpt, 0, 0.08), cfg.gpt, "cuda", dtype="bf16", max_kv=256)
+            _cache["eng"].PL_MAX_ROWS = 128  # every shape the kernel supports, whatever the product threshold
         finally:
             if old is None:
                 del os.environ["ITTS_PL"]
