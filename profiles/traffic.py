@@ -24,7 +24,7 @@ import sys
 
 DECODE_KERNELS = ("attn_decode_kernel", "decode_gemm_kernel", "decode_gemm16_kernel", "decode_gemm16x_kernel",
                   "residual_reduce_ln", "sample_embed_kernel", "sample_topk_embed_kernel", "advance_kernel",
-                  "gpt_layer_pl_kernel", "fillBuffer",  # persistent layers (r04) + the per-step counter memset
+                  "gpt_layer_pl_kernel", "pl_zero_kernel",  # persistent layers (r04) + the per-step counter reset
                   "beam_cand_kernel", "beam_select_kernel")
 
 
