@@ -15,10 +15,10 @@ from indextts.utils.synthetic import gpt_state_dict  # noqa: E402
 
 NAMES = ["start", "A0 issued", "A c_attn", "E1 q/k/v in", "B attention", "E2 o ready", "C c_proj",
          "E3 part ready", "D x1", "E4 x1 ready", "E c_fc", "E5 f ready", "F mlp.c_proj", "E6 part ready",
-         "G end", "E2 drained", "E3 drained", "E4 drained", "E5 drained", "E6 drained"]
+         "G end", "E2 drained", "E3 drained", "E4 drained", "E5 drained", "E6 drained", "B keys done"]
 
 
-def run(eng, B, L_text=48, steps=40):
+def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
     g = torch.Generator().manual_seed(3)
     text = torch.randint(2, 12000, (B, L_text), generator=g).cuda()
     conds = torch.randn(B, 32, 1024, generator=g).cuda()
@@ -28,12 +28,12 @@ def run(eng, B, L_text=48, steps=40):
     torch.cuda.synchronize()
     OFF_TRACE = int(eng.lib.itts_gpt_pl_scratch_bytes()) - 256 - 256 * 32 * 8
     tr = eng._pl_scratch.view(torch.uint8)[OFF_TRACE:OFF_TRACE + 256 * 32 * 8].view(torch.int64).view(256, 32)
-    tr = tr[:, :20].cpu().double()
+    tr = tr[:, :21].cpu().double()
     t0 = tr[:, 0].min()
     rel = (tr - t0) / 100.0  # 100 MHz -> µs
-    print(f"B={B}: layer span {float(rel[:, 14].max()):.2f} us (first start -> last end)")
+    print(f"B={B}, {steps} steps (keys at the traced step: {32 + L_text + 2 + steps}): layer span {float(rel[:, 14].max()):.2f} us (first start -> last end)")
     prev = None
-    order = [0, 1, 2, 3, 4, 15, 5, 6, 16, 7, 8, 17, 9, 10, 18, 11, 12, 19, 13, 14]
+    order = [0, 1, 2, 3, 20, 4, 15, 5, 6, 16, 7, 8, 17, 9, 10, 18, 11, 12, 19, 13, 14]
     for i in order:
         n = NAMES[i]
         col = rel[:, i]
