@@ -483,7 +483,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           xv[2 * i + 1] = __uint_as_float(r[i] & 0xFFFF0000u);
         }
       };
-      for (int j0 = 0; j0 < nk; j0 += NG * kKB) {
+      // one round of kKB keys per group; round 0 is peeled out of the loop: in straight-line code the
+      // compiler waits only for this round's K/V rows (issued at launch start), whereas a loop header
+      // waits for every load in flight -- here also the weight DMA issued after the q/k/v sweep
+      auto key_round = [&](int j0) __attribute__((always_inline)) {
         const bool more = j0 + NG * kKB < nk;
         float sc[kKB];
 #pragma unroll
@@ -530,7 +533,9 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           m_run = mn;
         }
         if (more) kv_load(vr, p.vc, rr, p0, nk, j0 + NG * kKB);
-      }
+      };
+      key_round(0);  // nk >= 1: round 0 always runs
+      for (int j0 = NG * kKB; j0 < nk; j0 += NG * kKB) key_round(j0);
       if (pt == 0) mark(20);
 #pragma unroll
       for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
