@@ -328,7 +328,7 @@ def main():
         pl = bool(tts.gpt.pl and tts.gpt._pl_ok({"B": rows}))
         body = ("20 x ONE persistent launch per layer (gpt_layer.hip: c_attn (ln_1 folded) -> attention -> "
                 "attn.c_proj split-K 8 + reduce -> c_fc (ln_2 folded, gelu) -> mlp.c_proj split-K 8 + reduce as "
-                "phases joined by in-launch hand-offs, weights prefetched by LDS-DMA) + counter memset + "
+                "phases joined by in-launch hand-offs, weights prefetched by LDS-DMA) + counter reset kernel + "
                 "last-layer reduce/ln_f/final_norm" if pl else
                 "20 x [c_attn GEMM (ln_1 folded), attention, attn.c_proj GEMM split-K 8, reduce, c_fc GEMM "
                 "(ln_2 folded, gelu), mlp.c_proj GEMM (split-K 8), reduce]")
