@@ -79,6 +79,11 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 #define PL_SCOPE __HIP_MEMORY_SCOPE_AGENT
 #define PL_AUX 16
 #endif
+// ITTS_PL_KV_LATE=1: pass 0's K/V rows are requested after the c_attn MFMAs (A/B: they queue in front of
+// nothing the critical path needs, but start later)
+#ifndef ITTS_PL_KV_LATE
+#define ITTS_PL_KV_LATE 0
+#endif
 #ifndef ITTS_PL_DMA_EARLY
 #define ITTS_PL_DMA_EARLY 0
 #endif
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
     }
     __builtin_amdgcn_sched_barrier(0);
-    {
+    if (!ITTS_PL_KV_LATE) {
       const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
       const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
       kv_load(kr, p.kc, rr, p0, nk, 0);
@@ -398,6 +403,12 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       }
     }
     if (MT > 1) bar();  // red / statistics are reused by the next tile
+  }
+  if (ITTS_PL_KV_LATE) {  // pass 0's K/V rows behind the c_attn operands instead of right after them
+    const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
+    const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+    kv_load(kr, p.kc, rr, p0, nk, 0);
+    kv_load(vr, p.vc, rr, p0, nk, 0);
   }
   mark(2);
 
