@@ -47,7 +47,10 @@ constexpr int kNC = 8, kCPC = 32, kWG = kNC * kCPC;  // clusters, workgroups per
 constexpr int kNW = 8;                                // compute waves
 constexpr int kThreads = kNW * 64;
 constexpr int kQC = 12;                               // c_attn columns per workgroup
-constexpr int kKB = 8;                                // attention keys per group per round (load depth)
+#ifndef ITTS_PL_KB
+#define ITTS_PL_KB 8
+#endif
+constexpr int kKB = ITTS_PL_KB;  // attention keys per group per round (load depth; results do not depend on it)
 constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
 constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s), then the grid drains
 // ITTS_PL_TRACE=1 (timing builds): wave 0 of every workgroup stamps the 100-MHz real-time counter at
