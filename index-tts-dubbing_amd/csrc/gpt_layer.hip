@@ -48,7 +48,7 @@ constexpr int kNW = 8;                                // compute waves
 constexpr int kThreads = kNW * 64;
 constexpr int kQC = 12;                               // c_attn columns per workgroup
 #ifndef ITTS_PL_KB
-#define ITTS_PL_KB 8
+#define ITTS_PL_KB 4  // 8: 666.5 us per C3 step, 4: 661.3, 12: 684 (profiles/lib_ab2.sh)
 #endif
 constexpr int kKB = ITTS_PL_KB;  // attention keys per group per round (load depth; results do not depend on it)
 constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
