@@ -84,6 +84,9 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 #endif
 // ITTS_PL_KV_LATE=1: pass 0's K/V rows are requested after the c_attn MFMAs (A/B: they queue in front of
 // nothing the critical path needs, but start later)
+#ifndef ITTS_PL_PART16
+#define ITTS_PL_PART16 0  // 16-B partial stores measured neutral: 663.0 vs 661.2 us per C3 step
+#endif
 #ifndef ITTS_PL_KV_LATE
 #define ITTS_PL_KV_LATE 0
 #endif
@@ -608,7 +611,30 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   mark(5);
   bar();
   if (*abort_flag) return;
-  auto store_partial = [&](float* dst, int t) {  // 1024 outputs of row tile t, 2 per thread, fixed-order sum
+  // 1024 outputs of row tile t, fixed-order sum over the waves; ITTS_PL_PART16=1: 4 consecutive
+  // columns per thread as ONE 16-B write-through store (256 threads) instead of 4-B stores (512 x 2; A/B, off:
+  // measured neutral, profiles/lib_ab2.sh): a
+  // narrow sc1 store is one fabric write each (MI355X_MICROARCH.md visibility table: dword ~6x the
+  // dwordx4 time per byte), and the drain before the counter add waits for all of them
+  auto store_partial = [&](float* dst, int t) {
+    if (ITTS_PL_PART16) {
+      if (tid < 256) {
+        const int o = 4 * tid;
+        float v4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ww = 0; ww < kNW; ++ww)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v4[k] += red[ww * 1024 + o + k];
+        const int r = o >> 6, l = o & 63;
+        const int row = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+        const u32x4_t pv4{__float_as_uint(v4[0]), __float_as_uint(v4[1]), __float_as_uint(v4[2]),
+                          __float_as_uint(v4[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(pv4, rs, (((c * kMaxR + row) * kD) + 32 * j + (l & 31)) * 4, 0,
+                                               PL_AUX);
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int o = tid + 512 * k;
