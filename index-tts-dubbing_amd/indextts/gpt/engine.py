@@ -884,7 +884,9 @@ class HipGPT:
     # decode steps per captured graph replay (ITTS_GRAPH_STEPS; 1 = one step per replay): 4 steps
     # per graph 776 vs 785 us per step (profiles/graph_steps_r02.txt: the boundary between two graph
     # launches costs more than a kernel boundary inside one graph)
-    GRAPH_STEPS = int(os.environ.get("ITTS_GRAPH_STEPS", "4"))
+    # round 4, persistent layers: 4 / 8 / 16 steps per replay 661.6 / 659.2 / 659.9 us per C3 step
+    # (profiles/env_ab2.sh, two interleaved reps each)
+    GRAPH_STEPS = int(os.environ.get("ITTS_GRAPH_STEPS", "8"))
 
     def _multi_graph(self, ln, n, min_new, penalty, gkey):
         """the lane's n-step graph (captured on first use, like the one-step graph)."""
