@@ -396,6 +396,25 @@ typedef struct ItTsSampling {
  * forced: caller's choice).  A host without Python allocates these and fills ItTsGptDecodeState. */
 #define ITTS_GPT_STATE_NBUF 14
 int itts_gpt_decode_state_bytes(const ItTsGptWeights* w, int rows, int max_kv, int max_new, int64_t* bytes);
+/* ---- weight packers (HOST memory in and out, CPU only: callable without a GPU) -------------------
+ * What ItTsGptLayerW / ItTsGptPlLayerW point at, built from the checkpoint tensors (HF Conv1D weights
+ * [in = K][out = N], gpt/model.py:255-281 -> modeling_gpt2.py:246-306; mel_head [V][D], gpt/model.py:48);
+ * copy the outputs to the device.  HipGPT packs through these same functions. */
+/* LayerNorm folded into the following linear layer: wt [N][K] bf16 = W'^T with W' = diag(ln_g) W (computed
+ * in double, rounded to f32, then to bf16), u [N] = column sums of the rounded W' (exact, in double),
+ * c [N] = ln_b^T W + bias (double).  ln_g = ln_b = NULL: wt = bf16(W^T), c = bias, u untouched.
+ * -> qkv_u / qkv_c (ln_1 -> c_attn), fc_u / fc_c (ln_2 -> c_fc), o_c (attn.c_proj, no LN). */
+int itts_gpt_fold_ln(const float* w_io, const float* bias, const float* ln_g, const float* ln_b, int K, int N,
+                     uint16_t* wt, float* u, float* c);
+/* MFMA fragment order of W^T [N][K] (f32 rounded to bf16, or bf16), N zero-padded to a multiple of cols:
+ * cols 16 -> [N/16][K/32][64][8], lane 16q + c holds W^T[16nt + c][32s + 8q : +8] (qkv_w16, o_w16, fc_w16);
+ * cols 32 -> [N/32][K/16][64][8], lane 32h + r holds W^T[32nt + r][16s + 8h : +8] (proj_w, o_w, head_w).
+ * out: ceil(N / cols) * cols * K bf16. */
+int itts_gpt_pack_frag(const void* wt, int wt_dtype, int N, int K, int cols, uint16_t* out);
+/* ItTsGptPlLayerW of one layer from c_attn's folded wt [3D][D] bf16 and its u / c (itts_gpt_fold_ln):
+ * workgroup b = 8j + c computes columns 12(j % 16) .. +11 of head h = 2c + j / 16's [q | k | v] 192;
+ * w12 [256][D/32][4][12][8] bf16, uc [256][2][12] f32.  D = 1024, H = 16 only. */
+int itts_gpt_pack_qkv12(const uint16_t* wt, const float* u, const float* c, int D, int H, uint16_t* w12, float* uc);
 /* ---- full-sequence passes (prefill, teacher-forced latent pass) ---------------------------------- */
 /* One GPT-2 block's weights for the sequence GEMMs: bf16 mode = the implicit-GEMM packing of W^T [N][K]
  * (itts_igemm_pack_dims, 1 tap), f32 mode = f32 W^T [N][K] (HF Conv1D [in][out] transposed). */
@@ -460,24 +479,35 @@ typedef struct ItTsGptPlLayerW {
   const void* qkv_w12;  /* c_attn (ln_1 folded), 12 columns per workgroup: [256][32][4][12][8] bf16 */
   const float* qkv_uc;  /* [256][2][12]: u and c of those columns (itts_decode_gemm16x fold terms) */
 } ItTsGptPlLayerW;
-/* Bytes of the device scratch the persistent layers share (hand-off buffers, counters and a sticky
- * error word); zero it once after allocation. */
+/* Bytes of the device scratch the persistent layers share (hand-off buffers, counters, the launch epoch
+ * and a sticky error word); zero it once after allocation (or call itts_gpt_pl_reset).  Nothing is reset
+ * between steps: every hand-off is tagged with the launch's epoch (ABI 4). */
 int64_t itts_gpt_pl_scratch_bytes(void);
-/* 1 if the persistent path runs this shape on the current device (256 CUs resident at once), else 0. */
+/* 1 if the persistent path runs this shape on the current device (256 CUs, one workgroup of each kernel
+ * instantiation resident per CU), else 0.  The grid needs every CU at once: run it with no other kernel
+ * on the device (a workgroup that cannot be placed makes the others time out, itts_gpt_pl_error). */
 int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows);
-/* Zero the step's hand-off counters and granules (a memset node); once before the layers of every step. */
-int itts_gpt_pl_begin_step(void* scratch, int rows, void* stream);
+/* Re-arm the scratch (counters, granules, epoch, error word := 0) with a kernel on `stream`: after an
+ * error reported by itts_gpt_pl_error, before the next persistent launch. */
+int itts_gpt_pl_reset(void* scratch, void* stream);
 /* Layer `layer` of decode step `kstep` of a multi-step call (key kv_base + t + kstep); `last`: leave
  * the mlp.c_proj reduce (+ ln_f + final_norm) to itts_residual_reduce_ln over the scratch partials. */
 int itts_gpt_layer_pl(const ItTsGptLayerW* layer_w, const ItTsGptPlLayerW* pl, const ItTsGptDecodeState* state,
                       int layer, int kstep, int last, void* scratch, void* stream);
 /* A hand-off timeout recorded in the scratch (0 = none; else every later layer launch returns at once
- * and the results are invalid until the scratch is zeroed again).  Synchronises `stream`. */
+ * and the results are invalid until itts_gpt_pl_reset; the launch chain, itts_gpt_decode_steps, gives
+ * the same results bit for bit and needs no scratch).  Synchronises `stream`. */
 int itts_gpt_pl_error(const void* scratch, void* stream, int* code);
 /* itts_gpt_decode_steps with every layer on the persistent path (pl: [n_layer]); sampling mode 2 (beams:
  * logits only, nsteps = 1, the caller runs the beam kernels and the step advance) as itts_gpt_decode_step. */
 int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPlLayerW* pl, void* scratch,
                              const ItTsGptDecodeState* state, const ItTsSampling* sampling, int nsteps, void* stream);
+
+/* ---- diagnostics ------------------------------------------------------------------------------ */
+/* n_wg workgroups that each hold 120 KiB of LDS (one per CU) for `usec` microseconds, then exit (sink: NULL
+ * or [n_wg] ints written at exit).  Test instrumentation: keeps CUs away from a persistent grid launched
+ * beside it, to exercise the hand-off timeout (itts_gpt_pl_error) and the launch-chain fallback. */
+int itts_diag_occupy(int n_wg, int usec, int* sink, void* stream);
 
 #ifdef __cplusplus
 }

@@ -36,8 +36,15 @@
 // payload stored sc1 (write-through), every storing wave s_waitcnt vmcnt(0), workgroup barrier, ONE
 // lane adds to the counter (relaxed, agent scope); the consumer polls relaxed with s_sleep, every load
 // of handed-off bytes is an sc1 load.  Every spin is bounded: a timeout sets an error word and the
-// whole grid drains (results then garbage, the host reports the error); counters and granules are
-// zeroed by a memset node before every step.
+// whole grid drains (results then garbage, the host reports the error and re-arms the scratch with
+// itts_gpt_pl_reset).
+// Epochs (round 5): nothing is reset between steps.  Launch number E (a u32 in the scratch, E = seq + 1,
+// advanced by workgroup 0 once every workgroup of the launch has read it) tags every q/k/v granule, and
+// every hand-off counter only grows: after launch E a counter with n adders per launch holds n * E, so
+// the poll target is n * E (wrap-safe signed compare).  A value left by an earlier launch (a granule's
+// tag, a counter line some cache kept) is below / unequal to this launch's and can never satisfy a
+// poll, whatever happened between the launches (round 4 zeroed them per step: as a memset node that let
+// 30 of 64 reused-lane cues decode wrong data).
 #include "common.h"
 
 namespace {
@@ -94,8 +101,8 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 #define ITTS_PL_DMA_EARLY 0
 #endif
 
-// scratch layout (bytes) for up to kMaxR rows; the counters and the granules of the step's rows are zeroed
-// before every step
+// scratch layout (bytes) for up to kMaxR rows; counters, granules, the epoch and the error word are zero after
+// itts_gpt_pl_reset (and after the caller's zero fill at allocation), never between steps
 constexpr int kMaxR = 128;
 // hand-off counters, one per 4-KiB block: 256 workgroups polling counters that share one line saturated
 // it (hand-offs observed 2.5-6 us after the last arrival, profiles/pl_trace_r04b.txt); ITTS_PL_CNT_STRIDE=1
@@ -113,9 +120,10 @@ constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * kMaxR * kD * 4;    // [8][128
 constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * kMaxR * kD * 2;    // [8][128][512] bf16
 constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * kMaxR * 512 * 2;   // [8][128][1024] f32
 constexpr int64_t kOffTrace = kOffP2 + (int64_t)kNC * kMaxR * kD * 4; // [256 WG][32] u64 (ITTS_PL_TRACE builds)
-constexpr int64_t kOffErr = kOffTrace + (int64_t)kWG * 32 * 8;        // sticky error word (not zeroed per step)
+constexpr int64_t kOffSeq = kOffTrace + (int64_t)kWG * 32 * 8;        // u32 epoch: launches since the reset
+constexpr int64_t kOffErr = kOffSeq + 256;                             // sticky error word
 constexpr int64_t kScratchBytes = kOffErr + 256;
-inline int64_t zero_bytes(int rows) { return kOffGq + (int64_t)rows * kH * 192 * 8; }  // multiple of 16
+constexpr int64_t kZeroBytes = kOffGq + (int64_t)kMaxR * kH * 192 * 8;  // counters + every granule (x16)
 enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56 };
 
 // LDS layout (bytes)
@@ -178,10 +186,11 @@ __device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, PL_SCOPE);
 }
 
-// one lane polls `ctr` until >= target (bounded); returns false on timeout / a failed grid
+// one lane polls `ctr` until it reaches target (bounded; counters only grow, so the compare is the wrap-safe
+// signed difference); returns false on timeout / a failed grid
 __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uint32_t code) {
   for (uint32_t n = 0;; ++n) {
-    if (ld_relaxed(ctr) >= target) {
+    if ((int32_t)(ld_relaxed(ctr) - target) >= 0) {
       if (ITTS_PL_ACQ) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -209,9 +218,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = j >> 4, jj = j & 15, h = 2 * c + hh;
-  const uint32_t L1 = (uint32_t)p.layer + 1;  // epoch: counters / granules grow by one per layer
   uint32_t* cnt = reinterpret_cast<uint32_t*>(p.scratch + kOffCnt);
   uint32_t* err = reinterpret_cast<uint32_t*>(p.scratch + kOffErr);
+  uint32_t* seq = reinterpret_cast<uint32_t*>(p.scratch + kOffSeq);
+  // this launch's epoch (first needed at the end of phase A: the load's latency hides behind the operands)
+  const uint32_t L1 = ld_relaxed(seq) + 1u;
   // (no err check here: it cost a memory round trip before the first load; every poll and granule sweep
   // checks err every 256 spins, so after a timeout the grid still drains within one spin round per phase)
   uint64_t* gq = reinterpret_cast<uint64_t*>(p.scratch + kOffGq);
@@ -703,6 +714,9 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 
   // ---- (E) c_fc (ln_2 folded) + gelu on column tile 32c + j, per row tile, A = the cluster's x1^
   if (tid == 0 && !poll_ge(cnt + (CNT4 + c) * kCntStride, kCPC * L1, err, 4)) *abort_flag = 1;
+  // past this poll every workgroup of the grid has added at E3 (cluster c's 32 E4 adders each waited for
+  // the 8 clusters of its tile), so all have read the epoch: workgroup 0 advances it for the next launch
+  if (b == 0 && tid == 0 && !*abort_flag) st_sc1_u32(seq, L1);
   mark(9);
   bar();
   if (*abort_flag) return;
@@ -852,9 +866,23 @@ extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       n = 0;
-    g_cu_count = n;
+    // every instantiation must fit one workgroup per CU (LDS, registers): the grid is one per CU
+    int occ = 1;
+    const void* ks[] = {reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false>),
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, true>),
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, false>),
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, true>)};
+    for (const void* k : ks) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess || nb < 1) occ = 0;
+    }
+    (void)hipGetLastError();
+    g_cu_count = occ ? n : 0;
   }
-  return g_cu_count >= kWG ? 1 : 0;  // every workgroup must be resident at once (one per CU)
+  // every workgroup must be resident at once (one per CU); the caller must also keep other work off the
+  // device's CUs while a layer runs: a workgroup that cannot be placed makes the
+  // resident ones time out (itts_gpt_pl_error), never hang
+  return g_cu_count >= kWG ? 1 : 0;
 }
 
 extern "C" int itts_gpt_pl_error(const void* scratch, void* stream, int* code) {
@@ -936,31 +964,29 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   return itts::check_launch(fn);
 }
 
-// zero the step's counters and the granules of its rows (one memset node ahead of the layer launches)
-// ITTS_PL_ZERO_KERNEL=1 (default): the step's counters / granules are zeroed by this kernel, an ordinary
-// kernel node in a captured graph (=0: hipMemsetAsync, a memset node, kept as the A/B form)
-#ifndef ITTS_PL_ZERO_KERNEL
-#define ITTS_PL_ZERO_KERNEL 1
-#endif
+// Re-arm the scratch: counters, every granule, the epoch and the error word to zero.  An ordinary kernel
+// (the stores go through the caches like any kernel's), needed only after an error: a timeout leaves the
+// counters short of their epoch.  Never per step (the epochs make stale values harmless).
 namespace {
-__global__ __launch_bounds__(256) void pl_zero_kernel(u32x4_t* p, int64_t n16) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256)
-    p[i] = u32x4_t{0u, 0u, 0u, 0u};
+__global__ __launch_bounds__(256) void pl_zero_kernel(u32x4_t* p, int64_t n16, u32x4_t* tail, int64_t t16) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16 + t16; i += (int64_t)gridDim.x * 256) {
+    if (i < n16)
+      p[i] = u32x4_t{0u, 0u, 0u, 0u};
+    else
+      tail[i - n16] = u32x4_t{0u, 0u, 0u, 0u};
+  }
 }
 }  // namespace
 
-extern "C" int itts_gpt_pl_begin_step(void* scratch, int rows, void* stream) {
-  const char* fn = "itts_gpt_pl_begin_step";
-  ITTS_REQUIRE(scratch && rows >= 1 && rows <= kMaxR, fn, "null scratch or rows outside 1..128");
-  const int64_t n16 = zero_bytes(rows) / 16;
-  if (ITTS_PL_ZERO_KERNEL) {
-    const int blocks = (int)((n16 + 255) / 256 < 1024 ? (n16 + 255) / 256 : 1024);
-    hipLaunchKernelGGL(pl_zero_kernel, dim3(blocks), dim3(256), 0, itts::as_stream(stream),
-                       static_cast<u32x4_t*>(scratch), n16);
-    return itts::check_launch(fn);
-  }
-  if (hipMemsetAsync(scratch, 0, zero_bytes(rows), itts::as_stream(stream)) != hipSuccess) return itts::check_launch(fn);
-  return 0;
+extern "C" int itts_gpt_pl_reset(void* scratch, void* stream) {
+  const char* fn = "itts_gpt_pl_reset";
+  ITTS_REQUIRE(scratch, fn, "null scratch");
+  ITTS_REQUIRE((reinterpret_cast<uintptr_t>(scratch) & 255) == 0, fn, "scratch must be 256-B aligned");
+  unsigned char* s = static_cast<unsigned char*>(scratch);
+  const int64_t n16 = kZeroBytes / 16, t16 = (kScratchBytes - kOffSeq) / 16;
+  hipLaunchKernelGGL(pl_zero_kernel, dim3(1024), dim3(256), 0, itts::as_stream(stream), reinterpret_cast<u32x4_t*>(s),
+                     n16, reinterpret_cast<u32x4_t*>(s + kOffSeq), t16);
+  return itts::check_launch(fn);
 }
 
 extern "C" int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPlLayerW* pl, void* scratch,
@@ -977,7 +1003,6 @@ extern "C" int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPl
   const int L = w->n_layer, D = w->d_model, R = st->rows;
   int rc = 0;
   for (int k = 0; k < nsteps && rc == 0; ++k) {
-    rc = itts_gpt_pl_begin_step(scratch, R, stream);
     for (int l = 0; l < L && rc == 0; ++l)
       rc = itts_gpt_layer_pl(&w->layers[l], &pl[l], st, l, k, l + 1 == L, scratch, stream);
     // the last layer's mlp.c_proj reduce with ln_f + final_norm (Q5) over the persistent partials

@@ -89,16 +89,20 @@ SIGNATURES = {
                                      _c_i, _vp, _c_i, _vp, _c_i, _vp, _vp]),
     "itts_gpt_prefill": (_c_i, [_vp, _vp, _vp, _vp, _c_i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "itts_gpt_decode_state_bytes": (_c_i, [_vp, _c_i, _c_i, _c_i, _vp]),
+    "itts_gpt_fold_ln": (_c_i, [_vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _vp]),
+    "itts_gpt_pack_frag": (_c_i, [_vp, _c_i, _c_i, _c_i, _c_i, _vp]),
+    "itts_gpt_pack_qkv12": (_c_i, [_vp, _vp, _vp, _c_i, _c_i, _vp, _vp]),
     "itts_gpt_decode_step": (_c_i, [_vp, _vp, _vp, _vp]),
     "itts_gpt_decode_steps": (_c_i, [_vp, _vp, _vp, _c_i, _vp]),
     "itts_gpt_pl_scratch_bytes": (_c_i64, []),
     "itts_gpt_pl_supported": (_c_i, [_vp, _c_i]),
-    "itts_gpt_pl_begin_step": (_c_i, [_vp, _c_i, _vp]),
+    "itts_gpt_pl_reset": (_c_i, [_vp, _vp]),
     "itts_gpt_layer_pl": (_c_i, [_vp, _vp, _vp, _c_i, _c_i, _c_i, _vp, _vp]),
     "itts_gpt_pl_error": (_c_i, [_vp, _vp, ctypes.POINTER(_c_i)]),
     "itts_gpt_decode_steps_pl": (_c_i, [_vp, _vp, _vp, _vp, _vp, _c_i, _vp]),
     "itts_bigvgan_workspace_bytes": (_c_i64, [_vp, _c_i, _c_i]),
     "itts_bigvgan_forward": (_c_i, [_vp, _vp, _vp, _vp, _c_i, _c_i, _vp, _vp, _vp, _vp]),
+    "itts_diag_occupy": (_c_i, [_c_i, _c_i, _vp, _vp]),
 }
 
 

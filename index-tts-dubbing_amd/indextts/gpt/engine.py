@@ -15,9 +15,11 @@ done flags, codes) lives on the device so one captured hipGraph replays every st
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 import os
+import warnings
 from typing import List, Optional
 
 import numpy as np
@@ -31,70 +33,80 @@ def _t(v):
     return v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
 
 
+def _host(v, dtype=torch.float32):
+    """contiguous CPU copy (the packers are host functions of the C ABI)"""
+    return _t(v).detach().to("cpu", dtype).contiguous()
+
+
+def _ptr_or_none(t):
+    return None if t is None else t.data_ptr()
+
+
+def pack_frag(w_t, cols: int) -> torch.Tensor:
+    """W^T [N, K] (f32, rounded to bf16 here, or bf16) -> MFMA fragment order on the host through
+    itts_gpt_pack_frag (include/itts_hip.h): cols 32 -> [N/32][K/16][64 lanes][8] (lane 32h + r holds
+    W^T[32nt + r][16s + 8h : +8]), cols 16 -> [N/16][K/32][64][8] (lane 16q + c holds W^T[16nt + c][32s + 8q
+    : +8]); N zero-padded to a multiple of cols."""
+    lib = _hip.load()
+    w = _t(w_t).detach().cpu()
+    w = w.contiguous() if w.dtype == torch.bfloat16 else w.float().contiguous()
+    N, K = w.shape
+    ks = 16 if cols == 32 else 32
+    assert K % ks == 0
+    Np = (N + cols - 1) // cols * cols
+    out = torch.empty(Np * K, dtype=torch.bfloat16)
+    _hip.check(lib.itts_gpt_pack_frag(w.data_ptr(), _hip.BF16 if w.dtype == torch.bfloat16 else _hip.F32, N, K, cols,
+                                      out.data_ptr()), "itts_gpt_pack_frag")
+    return out.view(Np // cols, K // ks, 64 // cols, cols, 8)
+
+
 def pack_skinny(w_t: torch.Tensor) -> torch.Tensor:
-    """W^T [N, K] f32 -> MFMA-fragment order [N/32][K/16][64 lanes][8] bf16 (lane = 32*h + r holds
-    W^T[32*nt + r][16*s + 8*h : +8]); N zero-padded to a multiple of 32."""
-    N, K = w_t.shape
-    assert K % 16 == 0
-    Np = (N + 31) // 32 * 32
-    w = torch.zeros(Np, K, dtype=torch.float32)
-    w[:N] = w_t.float()
-    w = w.reshape(Np // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
-    return w.to(torch.bfloat16)
+    """32-column fragment order (itts_decode_gemm; attn.c_proj / mlp.c_proj split-K, mel_head)."""
+    return pack_frag(w_t, 32)
 
 
 def pack_skinny16(w_t: torch.Tensor) -> torch.Tensor:
-    """W^T [N, K] f32 -> 16-column fragment order [N/16][K/32][64 lanes][8] bf16 for
-    itts_decode_gemm16 (lane = 16*q + c holds W^T[16*nt + c][32*s + 8*q : +8]); N zero-padded."""
-    N, K = w_t.shape
-    assert K % 32 == 0
-    Np = (N + 15) // 16 * 16
-    w = torch.zeros(Np, K, dtype=torch.float32)
-    w[:N] = w_t.float()
-    w = w.reshape(Np // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
-    return w.to(torch.bfloat16)
+    """16-column fragment order (itts_decode_gemm16 / 16x)."""
+    return pack_frag(w_t, 16)
 
 
-def fold_ln_weights(w_io, bias, ln, device):
+def fold_ln_weights(w_io, bias, ln, device, keep_wt: bool = False):
     """Operands of itts_decode_gemm16x for HF Conv1D weight ``w_io`` [in=K, out=N] (+ bias [N]) fed by
-    LayerNorm ``ln`` = (g, b) (None: no LayerNorm): W' = diag(g) W rounded to bf16 and packed on
-    16-column tiles, u = column sums of the ROUNDED W' (so the kernel's mean term cancels exactly what
-    its MFMAs accumulated), c = b^T W + bias (float64 accumulation)."""
-    w = _t(w_io).double()
-    bias = _t(bias).double()
-    if ln is None:
-        wt = w.t().float()
-        return {"w16": pack_skinny16(wt).to(device), "u": None, "c": bias.float().to(device),
-                "N": wt.shape[0], "K": wt.shape[1]}
-    g, b = _t(ln[0]).double(), _t(ln[1]).double()
-    wp = (w * g[:, None]).t().float().to(torch.bfloat16)  # W'^T [N, K]
-    u = wp.double().sum(1)
-    c = b @ w + bias
-    return {"w16": pack_skinny16(wp.float()).to(device), "u": u.float().to(device), "c": c.float().to(device),
-            "N": wp.shape[0], "K": wp.shape[1]}
+    LayerNorm ``ln`` = (g, b) (None: no LayerNorm), through itts_gpt_fold_ln: W' = diag(g) W rounded to
+    bf16 and packed on 16-column tiles, u = column sums of the ROUNDED W' (so the kernel's mean term
+    cancels exactly what its MFMAs accumulated), c = b^T W + bias (float64 accumulation).
+    keep_wt: also return the host bf16 W'^T [N, K] (pack_qkv12's input)."""
+    lib = _hip.load()
+    w, bs = _host(w_io), _host(bias)
+    K, N = w.shape
+    g, b = (None, None) if ln is None else (_host(ln[0]), _host(ln[1]))
+    wt = torch.empty(N, K, dtype=torch.bfloat16)
+    u = None if ln is None else torch.empty(N)
+    c = torch.empty(N)
+    _hip.check(lib.itts_gpt_fold_ln(w.data_ptr(), bs.data_ptr(), _ptr_or_none(g), _ptr_or_none(b), K, N, wt.data_ptr(),
+                                    _ptr_or_none(u), c.data_ptr()), "itts_gpt_fold_ln")
+    out = {"w16": pack_skinny16(wt).to(device), "u": None if u is None else u.to(device), "c": c.to(device),
+           "N": N, "K": K}
+    if keep_wt:
+        out["wt"], out["u_host"], out["c_host"] = wt, u, c
+    return out
 
 
-def pack_qkv12(wx_qkv, w_io, ln, n_head: int = 16):
-    """Persistent-layer c_attn operands (gpt_layer.hip): workgroup b = 8j + c computes 12 columns of
-    head h = 2c + j/16 -- columns 12*(j%16) .. +11 of that head's [q | k | v] 192 -- from the SAME
-    rounded W' = diag(ln_1.g) W and fold terms u / c as itts_decode_gemm16x (``wx_qkv`` from
-    fold_ln_weights), in 16x16x32 B-fragment order without the 4 unused columns:
+def pack_qkv12(wx_qkv, n_head: int = 16):
+    """Persistent-layer c_attn operands (gpt_layer.hip) through itts_gpt_pack_qkv12: workgroup b = 8j + c
+    computes 12 columns of head h = 2c + j/16 -- columns 12*(j%16) .. +11 of that head's [q | k | v] 192 --
+    from the SAME rounded W' = diag(ln_1.g) W and fold terms u / c as itts_decode_gemm16x (``wx_qkv`` from
+    fold_ln_weights(..., keep_wt=True)), in 16x16x32 B-fragment order without the 4 unused columns:
     W12 [256][32 k-steps][4][12][8] bf16, uc [256][2][12] f32."""
-    w = _t(w_io).double()
-    g = _t(ln[0]).double()
-    wp = (w * g[:, None]).t().float().to(torch.bfloat16)  # W'^T [3D, D], as fold_ln_weights rounds it
-    N, K = wp.shape
-    D = N // 3
-    b = torch.arange(256)
-    cl, j = b % 8, b // 8
-    h = 2 * cl + j // 16
-    i = 12 * (j % 16)[:, None] + torch.arange(12)[None, :]          # [256, 12] index in the head's 192
-    cols = (i // 64) * D + h[:, None] * 64 + i % 64                   # c_attn output column
-    w12 = wp[cols.reshape(-1)].reshape(256, 12, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+    lib = _hip.load()
+    wt = wx_qkv["wt"]
+    N, K = wt.shape
+    w12 = torch.empty(256, K // 32, 4, 12, 8, dtype=torch.bfloat16)
+    uc = torch.empty(256, 2, 12)
+    _hip.check(lib.itts_gpt_pack_qkv12(wt.data_ptr(), wx_qkv["u_host"].data_ptr(), wx_qkv["c_host"].data_ptr(), K,
+                                       n_head, w12.data_ptr(), uc.data_ptr()), "itts_gpt_pack_qkv12")
     dev = wx_qkv["u"].device
-    cd = cols.to(dev)
-    uc = torch.stack([wx_qkv["u"][cd], wx_qkv["c"][cd]], 1).contiguous()  # the exact f32 fold terms
-    return {"w12": w12.to(dev), "uc": uc}
+    return {"w12": w12.to(dev), "uc": uc.to(dev)}
 
 
 # the persistent decode layers are the default (C3 decode step 710 vs 765 us on the launch chain,
@@ -174,9 +186,11 @@ class HipGPT:
                     ly.wx[n] = fold_ln_weights(sd[f"{p}.{k}.weight"], sd[f"{p}.{k}.bias"],
                                                None if ln is None else (sd[f"{p}.ln_{1 if n == 'qkv' else 2}.weight"],
                                                                         sd[f"{p}.ln_{1 if n == 'qkv' else 2}.bias"]),
-                                               dev)
-            if self.pl:
-                ly.pl = pack_qkv12(ly.wx["qkv"], sd[f"{p}.attn.c_attn.weight"], (sd[f"{p}.ln_1.weight"], None))
+                                               dev, keep_wt=n == "qkv")
+                if self.pl:
+                    ly.pl = pack_qkv12(ly.wx["qkv"], self.H)
+                for key in ("wt", "u_host", "c_host"):
+                    ly.wx["qkv"].pop(key, None)
             if self.fuse_o:  # attn.c_proj in HF Conv1D [in, out] order (bf16) for the fused attention
                 ly.wo_io = sd[f"{p}.attn.c_proj.weight"].float().to(torch.bfloat16).contiguous().to(dev)
             self.layers.append(ly)
@@ -188,8 +202,12 @@ class HipGPT:
             self._plw = (_hip.GptPlLayerW * self.L)(*[_hip.GptPlLayerW(ly.pl["w12"].data_ptr(), ly.pl["uc"].data_ptr())
                                                      for ly in self.layers])
             n = int(self.lib.itts_gpt_pl_scratch_bytes())
-            self._pl_scratch = torch.zeros(n // 4 + 64, dtype=torch.float32, device=dev)  # 256-B aligned base
-            self._pl_err = self._pl_scratch[n // 4 - 64:]  # the sticky error word's block (re-armed per generate)
+            # zero-filled = armed (epoch 0); never reset between steps or calls, only after a hand-off
+            # timeout (_pl_recover).  torch's allocations are 256-B aligned.
+            self._pl_scratch = torch.zeros(n // 4 + 64, dtype=torch.float32, device=dev)
+        self._pl_block = 0     # > 0: decode on the launch chain (launch_chain(); another grid may share the CUs)
+        self._pl_strikes = 0   # hand-off timeouts so far; PL_MAX_STRIKES of them turn the persistent path off
+        self._pl_ran = False   # the last generate ran persistent layers (their error word is checked after it)
         self._lanes = {}  # lane index -> decode state, captured graph, stream
         self.step_events = None  # set to a list to time every decode step with HIP events (bench.py)
         self.logits_trace = None  # set to a list to record every step's raw logits [B, V] (tests)
@@ -510,10 +528,27 @@ class HipGPT:
     # vs bench_r04a_b3_pl0.json), so beams and the 128-row long-form chunks stay on the chain
     PL_MAX_ROWS = int(os.environ.get("ITTS_PL_MAX_ROWS", "32"))
 
+    @property
+    def pl_active(self):
+        """persistent layers enabled and not held off by launch_chain()"""
+        return self.pl and self._pl_block == 0
+
+    @contextlib.contextmanager
+    def launch_chain(self):
+        """Decode on the launch chain inside this block.  The persistent grid needs all 256 CUs at once
+        (one workgroup per CU): callers that run other kernels beside the decode (synthesize_many's back
+        stream) hold it off; results are bit-identical either way."""
+        self._pl_block += 1
+        try:
+            yield
+        finally:
+            self._pl_block -= 1
+
     def _pl_ok(self, st):
-        """persistent layers for this state: <= PL_MAX_ROWS (<= 128) rows, a 256-CU device, and no other
-        lane of this engine decoding concurrently (two persistent grids could each hold part of the CUs)"""
-        return (self.pl and st["B"] <= min(self.PL_MAX_ROWS, 128) and not st.get("multi_lane", False)
+        """persistent layers for this state: <= PL_MAX_ROWS (<= 128) rows, a 256-CU device with room for one
+        workgroup per CU, not held off, and no other lane of this engine decoding concurrently (two
+        persistent grids could each hold part of the CUs)"""
+        return (self.pl_active and st["B"] <= min(self.PL_MAX_ROWS, 128) and not st.get("multi_lane", False)
                 and bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), st["B"])))
 
     def pl_error(self):
@@ -524,6 +559,32 @@ class HipGPT:
         _hip.check(self.lib.itts_gpt_pl_error(self._pl_scratch.data_ptr(), _hip.stream_ptr(), ctypes.byref(code)),
                    "itts_gpt_pl_error")
         return int(code.value)
+
+    PL_MAX_STRIKES = 3
+
+    def _pl_recover(self, code):
+        """after a hand-off timeout (some workgroup could not be placed: another grid held CUs): re-arm the
+        scratch; the caller re-runs the call on the launch chain.  PL_MAX_STRIKES timeouts switch the
+        persistent path off for this engine."""
+        _hip.check(self.lib.itts_gpt_pl_reset(self._pl_scratch.data_ptr(), _hip.stream_ptr()), "itts_gpt_pl_reset")
+        self._pl_strikes += 1
+        off = self._pl_strikes >= self.PL_MAX_STRIKES
+        warnings.warn(f"persistent decode layer: hand-off timeout (code {code}); re-running this call on the launch "
+                      f"chain{' and keeping it off from now on' if off else ''} (results are identical)",
+                      RuntimeWarning, stacklevel=3)
+        if off:
+            self.pl = False
+
+    def _with_pl_fallback(self, fn, *args, **kw):
+        self._pl_ran = False
+        out = fn(*args, **kw)
+        if self._pl_ran:
+            code = self.pl_error()
+            if code:
+                self._pl_recover(code)
+                with self.launch_chain():
+                    out = fn(*args, **kw)
+        return out
 
     def _decode_step_fold(self, st, min_new, penalty):
         """bf16 product decode step, five launches per layer: c_attn (ln_1 folded) -> attention ->
@@ -735,13 +796,19 @@ class HipGPT:
             return self.generate_beam(conds, text_ids, max_new_tokens, num_beams, repetition_penalty,
                                       length_penalty, min_new_tokens, do_sample, temperature, top_k, top_p, seed,
                                       use_graph, check_every)
+        if do_sample and seed is None:  # drawn once: a re-run on the launch chain makes the same draws
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        return self._with_pl_fallback(self._generate, conds, text_ids, max_new_tokens, repetition_penalty,
+                                      min_new_tokens, use_graph, check_every, forced_codes, do_sample, temperature,
+                                      top_k, top_p, seed, lanes)
+
+    def _generate(self, conds, text_ids, max_new_tokens, repetition_penalty, min_new_tokens, use_graph, check_every,
+                  forced_codes, do_sample, temperature, top_k, top_p, seed, lanes):
         emb, pad, s = self.prepare_inputs(conds, text_ids)
         B = emb.shape[0]
         assert s + 1 + max_new_tokens <= self.max_kv, "KV capacity exceeded"
         sampling = (float(temperature), int(top_k), float(top_p)) if do_sample else None
-        if do_sample and seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None, self.cstep, self.pl)
+        gkey = (min_new_tokens, repetition_penalty, sampling, forced_codes is not None, self.cstep, self.pl_active)
         main = torch.cuda.current_stream(self.dev)
         work = []
         bounds = self._lane_bounds(B, lanes)
@@ -756,6 +823,7 @@ class HipGPT:
                                  None if forced_codes is None else forced_codes[r0:r1], min_new_tokens,
                                  repetition_penalty, use_graph and max_new_tokens > 1, gkey)
             work.append(ln)
+        self._pl_ran = any(self._pl_ok(ln["st"]) for ln in work)
         steps = 1
         trace = self.logits_trace  # optional instrumentation (tests): raw f32 logits of every step
         assert trace is None or len(work) == 1, "logits tracing needs a single lane"
@@ -800,11 +868,6 @@ class HipGPT:
                     break
         for ln in work:
             main.wait_stream(ln["stream"])
-            if self.pl and self._pl_ok(ln["st"]):
-                with torch.cuda.stream(ln["stream"]):
-                    code = self.pl_error()
-                if code:
-                    raise _hip.HipError(f"persistent decode layer: hand-off timeout (code {code})")
         codes = torch.cat([ln["st"]["codes"][:, :steps] for ln in work], 0).long()
         hit = codes == self.stop_mel
         if bool(hit.any(dim=1).all()):
@@ -817,8 +880,6 @@ class HipGPT:
         st = ln["st"]
         B = st["B"]
         st["s"] = s
-        if self.pl:
-            self._pl_err.zero_()
         st["pad"].copy_(pad)  # never rebind: the captured graph holds this pointer
         st["seen"].zero_()
         st["seen"][:, 1] = 1
@@ -991,18 +1052,23 @@ class HipGPT:
         -> codes [B, n] int64 (best hypothesis, then the stop token, padded with it)."""
         K = int(num_beams)
         assert 2 <= K <= 16, "num_beams must be in [2, 16]"
+        if do_sample and seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        return self._with_pl_fallback(self._generate_beam, conds, text_ids, max_new_tokens, K, repetition_penalty,
+                                      length_penalty, min_new_tokens, do_sample, temperature, top_k, top_p, seed,
+                                      use_graph, check_every)
+
+    def _generate_beam(self, conds, text_ids, max_new_tokens, K, repetition_penalty, length_penalty, min_new_tokens,
+                       do_sample, temperature, top_k, top_p, seed, use_graph, check_every):
         emb, pad, s = self.prepare_inputs(conds, text_ids)
         B = emb.shape[0]
         R = B * K
         assert s + 1 + max_new_tokens <= self.max_kv, "KV capacity exceeded"
         sampling = (float(temperature), int(top_k), float(top_p)) if do_sample else None
-        if do_sample and seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         ln = self._beam_state(B, K, max_new_tokens, s)
         st = ln["st"]
         st["s"] = s
-        if self.pl:
-            self._pl_err.zero_()
+        self._pl_ran = self._pl_ok(st)
         st["beam"] = {"K": K, "sampling": sampling, "min_new": min_new_tokens, "penalty": repetition_penalty,
                       "length_penalty": length_penalty}
         rows_b = torch.arange(B, device=self.dev).repeat_interleave(K)
@@ -1036,7 +1102,7 @@ class HipGPT:
         else:
             self._dgw(st["h"], self.head_w, R, self.head_b, st["logits"])
         self._beam_step(st, 0)
-        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep, self.pl)
+        gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep, self.pl_active)
         graph_ok = use_graph and max_new_tokens > 1
         if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
             ln["graph"] = (self._capture(st, min_new_tokens, repetition_penalty), gkey)
@@ -1067,8 +1133,6 @@ class HipGPT:
             steps += n
             if steps // check_every != prev // check_every and bool(st["done_u"].all()):
                 break
-        if self._pl_ok(st) and self.pl_error():
-            raise _hip.HipError("persistent decode layer: hand-off timeout")
         return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
 
     def _beam_finalize(self, st, B, K, steps, max_new, length_penalty):

@@ -8,6 +8,7 @@ latent pass and the vocoder).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Dict, List, Optional, Sequence
 
@@ -203,9 +204,13 @@ class BatchedTTS:
                 ids = torch.full((B, L), self.stop_text, dtype=torch.long)
                 for b, t in enumerate(texts):
                     ids[b, : t.numel()] = t.reshape(-1).long()
-                codes = self.gpt.generate(conds, ids.to(dev), over.get("max_mel_tokens", max_mel_tokens),
-                                          repetition_penalty=repetition_penalty,
-                                          min_new_tokens=over.get("min_new_tokens", min_new_tokens), **sampling)
+                # from the second batch on the back stream may run the previous batch's latent pass and vocoder
+                # beside this decode: the persistent decode grid needs every CU at once (gpt_layer.hip), so
+                # those decodes run on the launch chain (bit-identical results)
+                with self.gpt.launch_chain() if bi > 0 else contextlib.nullcontext():
+                    codes = self.gpt.generate(conds, ids.to(dev), over.get("max_mel_tokens", max_mel_tokens),
+                                              repetition_penalty=repetition_penalty,
+                                              min_new_tokens=over.get("min_new_tokens", min_new_tokens), **sampling)
                 rows = codes.cpu().numpy()  # syncs the front stream only
             fixed = [torch.from_numpy(remove_long_silence(rows[b], self.stop)) for b in range(B)]
             fixed = [f if f.numel() > 0 else torch.tensor([self.stop]) for f in fixed]

@@ -283,3 +283,168 @@ def test_prefill_decode_latent_through_the_abi_only(size):
     for b in range(B):
         n = int(lat_n[b])
         assert torch.equal(lat[b, :n].cpu(), lat_want[b, :n].cpu()), b
+
+
+def _abi_pack_layers(lib, sd, L, D, H, dev, keep):
+    """ItTsGptLayerW / ItTsGptPlLayerW arrays built with the header's host packers only (itts_gpt_fold_ln,
+    itts_gpt_pack_frag, itts_gpt_pack_qkv12), as a host without Python would: host buffers in, device
+    copies out."""
+    from indextts import _hip
+
+    def host(v):
+        return _t(v).detach().float().cpu().contiguous()
+
+    def todev(t):
+        d = t.to(dev)
+        keep.append(d)
+        return d.data_ptr()
+
+    def fold(w_io, bias, ln):
+        w, b = host(w_io), host(bias)
+        K, N = w.shape
+        wt = torch.empty(N, K, dtype=torch.bfloat16)
+        u, c = torch.empty(N), torch.empty(N)
+        g = None if ln is None else host(ln[0])
+        bb = None if ln is None else host(ln[1])
+        _hip.check(lib.itts_gpt_fold_ln(w.data_ptr(), b.data_ptr(), None if g is None else g.data_ptr(),
+                                        None if bb is None else bb.data_ptr(), K, N, wt.data_ptr(),
+                                        u.data_ptr(), c.data_ptr()), "itts_gpt_fold_ln")
+        return wt, u, c
+
+    def frag(wt, dtype, cols):
+        N, K = wt.shape
+        Np = (N + cols - 1) // cols * cols
+        out = torch.empty(Np * K, dtype=torch.bfloat16)
+        _hip.check(lib.itts_gpt_pack_frag(wt.data_ptr(), dtype, N, K, cols, out.data_ptr()), "itts_gpt_pack_frag")
+        return out
+
+    layers = (_hip.GptLayerW * L)()
+    pls = (_hip.GptPlLayerW * L)()
+    for i in range(L):
+        p = f"gpt.h.{i}."
+        ln1 = (sd[p + "ln_1.weight"], sd[p + "ln_1.bias"])
+        ln2 = (sd[p + "ln_2.weight"], sd[p + "ln_2.bias"])
+        q_wt, q_u, q_c = fold(sd[p + "attn.c_attn.weight"], sd[p + "attn.c_attn.bias"], ln1)
+        o_wt, _, o_c = fold(sd[p + "attn.c_proj.weight"], sd[p + "attn.c_proj.bias"], None)
+        f_wt, f_u, f_c = fold(sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"], ln2)
+        proj_t = host(sd[p + "mlp.c_proj.weight"]).t().contiguous()
+        w12 = torch.empty(256 * (D // 32) * 4 * 12 * 8, dtype=torch.bfloat16)
+        uc = torch.empty(256 * 2 * 12)
+        _hip.check(lib.itts_gpt_pack_qkv12(q_wt.data_ptr(), q_u.data_ptr(), q_c.data_ptr(), D, H, w12.data_ptr(),
+                                           uc.data_ptr()), "itts_gpt_pack_qkv12")
+        layers[i] = _hip.GptLayerW(todev(frag(q_wt, _hip.BF16, 16)), todev(q_u), todev(q_c),
+                                   todev(frag(o_wt, _hip.BF16, 16)), todev(o_c), todev(frag(f_wt, _hip.BF16, 16)),
+                                   todev(f_u), todev(f_c), todev(frag(proj_t, _hip.F32, 32)),
+                                   todev(host(sd[p + "mlp.c_proj.bias"])), todev(frag(o_wt, _hip.BF16, 32)))
+        pls[i] = _hip.GptPlLayerW(todev(w12), todev(uc))
+    head = todev(frag(host(sd["mel_head.weight"]), _hip.F32, 32))
+    return layers, pls, head
+
+
+def test_persistent_decode_through_the_abi_only():
+    """The default decode path (itts_gpt_decode_steps_pl: every layer one persistent launch) driven through
+    the header alone -- weights packed by the host packers, the scratch sized by itts_gpt_pl_scratch_bytes and
+    zero-filled, prefill by itts_gpt_prefill, 8 steps per call -- at the full IndexTTS-1.5 size on a
+    left-padded batch: codes bit-identical to HipGPT's launch chain (ITTS_PL=0, Python launch sequences)."""
+    import os
+    from indextts import _hip
+    from indextts.gpt.engine import HipGPT
+    from indextts.utils.config import default_config_path, load_config
+    from indextts.utils.synthetic import gpt_state_dict
+    from indextts.vocoder.bigvgan import pack_taps
+
+    lib = _hip.load()
+    cfg = load_config(default_config_path()).gpt
+    sd = gpt_state_dict(cfg, 0, 0.08)
+    dev = "cuda"
+    D, H, L, V = int(cfg.model_dim), int(cfg.heads), int(cfg.layers), int(cfg.number_mel_codes)
+    Vp = (V + 15) // 16 * 16
+    start, stop = int(cfg.start_mel_token), int(cfg.stop_mel_token)
+    B, N = 6, 41
+    g = torch.Generator().manual_seed(15)
+    conds = torch.randn(B, 32, D, generator=g).cuda()
+    text = torch.randint(2, 6000, (B, 20), generator=g)
+    text[1, :7] = 1
+    text[4, :3] = 1
+    text = text.cuda()
+    old = os.environ.get("ITTS_PL")
+    os.environ["ITTS_PL"] = "0"
+    try:
+        eng = HipGPT(sd, cfg, dev, dtype="bf16")
+    finally:
+        if old is None:
+            del os.environ["ITTS_PL"]
+        else:
+            os.environ["ITTS_PL"] = old
+    eng.cseq = False
+    want = eng.generate(conds, text, N, min_new_tokens=N, repetition_penalty=10.0).cpu()
+    emb, pad, s = eng.prepare_inputs(conds, text)
+    torch.cuda.synchronize()
+    del eng
+    torch.cuda.empty_cache()
+
+    keep = []
+    layers, pls, head = _abi_pack_layers(lib, sd, L, D, H, dev, keep)
+
+    def dev32(v):
+        t = _t(v).float().contiguous().to(dev)
+        keep.append(t)
+        return t.data_ptr()
+
+    lnf = (dev32(sd["gpt.ln_f.weight"]), dev32(sd["gpt.ln_f.bias"]), dev32(sd["final_norm.weight"]),
+           dev32(sd["final_norm.bias"]))
+    w = _hip.GptWeights(L, D, H, V, Vp, start, stop, layers, *lnf, head, dev32(sd["mel_head.bias"]),
+                        dev32(sd["mel_embedding.weight"]), dev32(sd["mel_pos_embedding.emb.weight"]))
+    if not lib.itts_gpt_pl_supported(ctypes.byref(w), B):
+        pytest.skip("persistent layer not available on this device")
+    seq_layers = (_hip.GptSeqLayerW * L)()
+    for i in range(L):
+        p = f"gpt.h.{i}."
+        ig = []
+        for k in ("attn.c_attn", "attn.c_proj", "mlp.c_fc", "mlp.c_proj"):
+            wt = _t(sd[p + k + ".weight"]).float().t().contiguous()
+            t = pack_taps([wt], wt.shape[1], wt.shape[0]).to(dev)
+            keep.append(t)
+            ig.append(t.data_ptr())
+        seq_layers[i] = _hip.GptSeqLayerW(*ig, *[dev32(sd[p + k + ".bias"]) for k in
+                                                 ("attn.c_attn", "attn.c_proj", "mlp.c_fc", "mlp.c_proj")],
+                                          dev32(sd[p + "ln_1.weight"]), dev32(sd[p + "ln_1.bias"]),
+                                          dev32(sd[p + "ln_2.weight"]), dev32(sd[p + "ln_2.bias"]))
+    ws = _hip.GptSeqWeights(L, D, H, _hip.BF16, seq_layers, *lnf, None)
+    max_kv = s + 1 + N + 8
+    sizes = (ctypes.c_int64 * _hip.GPT_STATE_NBUF)()
+    assert lib.itts_gpt_decode_state_bytes(ctypes.byref(w), B, max_kv, N, sizes) == 0
+    buf = [torch.zeros(int(n), dtype=torch.uint8, device=dev) for n in sizes]
+    x, xh, qkv, o, f, part, logits, kc, vc, padb, tst, seen, done, codes = buf
+    padb.view(torch.int32).copy_(pad)
+    seen.view(B, Vp)[:, 1] = 1
+    seen.view(B, Vp)[:, start] = 1
+    codes.view(torch.int32).fill_(stop)
+    st = _hip.GptDecodeState(B, max_kv, s + 1, N, x.data_ptr(), xh.data_ptr(), qkv.data_ptr(), o.data_ptr(),
+                             f.data_ptr(), part.data_ptr(), logits.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                             padb.data_ptr(), tst.data_ptr(), None, 0, seen.data_ptr(), done.data_ptr(),
+                             codes.data_ptr(), None)
+    smp = _hip.Sampling(0, N, 10.0, 1.0, 0, 1.0)
+    scratch = torch.zeros(int(lib.itts_gpt_pl_scratch_bytes()), dtype=torch.uint8, device=dev)
+    assert scratch.data_ptr() % 256 == 0
+    stream = torch.cuda.current_stream().cuda_stream
+    M = B * (s + 1)
+    work = torch.empty(int(lib.itts_gpt_forward_rows_workspace_bytes(ctypes.byref(ws), M)), dtype=torch.uint8,
+                       device=dev)
+    xin = emb.reshape(M, D).contiguous()
+    starts = (torch.arange(B, dtype=torch.int32) * (s + 1)).to(dev)
+    lens = torch.full((B,), s + 1, dtype=torch.int32, device=dev)
+    _hip.check(lib.itts_gpt_prefill(ctypes.byref(ws), ctypes.byref(w), ctypes.byref(st), xin.data_ptr(), s,
+                                    starts.data_ptr(), lens.data_ptr(), (starts + s).contiguous().data_ptr(),
+                                    ctypes.byref(smp), work.data_ptr(), stream), "itts_gpt_prefill")
+    done_steps = 1
+    while done_steps < N:  # 8 steps per call while they fit, then single steps
+        n = 8 if done_steps + 8 <= N else 1
+        _hip.check(lib.itts_gpt_decode_steps_pl(ctypes.byref(w), pls, scratch.data_ptr(), ctypes.byref(st),
+                                                ctypes.byref(smp), n, stream), "itts_gpt_decode_steps_pl")
+        done_steps += n
+    code = ctypes.c_int(-1)
+    _hip.check(lib.itts_gpt_pl_error(scratch.data_ptr(), stream, ctypes.byref(code)), "itts_gpt_pl_error")
+    assert code.value == 0
+    got = codes.view(torch.int32).view(B, N).cpu().long()
+    assert torch.equal(got[:, : want.shape[1]], want), (got, want)
