@@ -11,10 +11,11 @@ the timed region starts; weights are seeded random-init IndexTTS-1.5 (no checkpo
 Also reports ``roofline``: the dominant unit of work, the hipGraph-replayed GPT decode step (>60 % of
 the step; HBM-bound): algorithmic bytes (every weight byte + the K/V rows attended) per replay /
 the replay's duration from HIP events recorded on the decode stream around each replay, and
-``traffic`` = measured HBM bytes per step from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-(profiles/run_profiles.sh -> profiles/traffic_decode_r01.json); ``roofline_vocoder_conv``: the MFMA
-implicit GEMM running the BigVGAN convs (HIP events around each launch); and ``cpu_baseline``: the
-fp32 oracle (a CPU restatement of the reference path) on a bounded sample, on this host's cores.
+``traffic`` = measured HBM bytes per step from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the
+current build (profiles/run_profiles_r05.sh -> the TRAFFIC_DECODE file below); ``roofline_vocoder_conv``:
+the MFMA implicit GEMM running the BigVGAN convs, and the HBM-bound vocoder kernels (activation, AMP
+convs, fused conv -> activation), from HIP events around each launch; and ``cpu_baseline``: the fp32
+oracle (a CPU restatement of the reference path) on a bounded sample, on this host's cores.
 """
 import argparse
 import json
@@ -37,8 +38,8 @@ PEAK_HBM_GBS = 8000.0
 # PMC traffic summaries of the CURRENT build (profiles/run_profiles.sh; FETCH_SIZE x2 per
 # MI355X_MICROARCH.md, calibrated by profiles/pmc_calibrate.py); None when not yet measured
 # per decoding and decode path (persistent layers or the launch chain): None until measured for this build
-TRAFFIC_DECODE = {("greedy", True): "traffic_decode_pl_r04.json", ("greedy", False): "traffic_decode_r04.json",
-                  ("beam3", True): "traffic_decode_beam3_pl_r04.json", ("beam3", False): "traffic_decode_beam3_r04.json"}
+TRAFFIC_DECODE = {("greedy", True): "traffic_decode_pl_r04j.json", ("greedy", False): "traffic_decode_r04.json",
+                  ("beam3", False): "traffic_decode_beam3_r04h.json"}
 TRAFFIC_VOCODER = "traffic_vocoder_r03s.json"
 
 
@@ -86,12 +87,13 @@ def install_conv_timer(voc, timer):
     voc._conv = timed
 
 
-def install_hbm_timers(voc, t_act, t_amp):
-    """HIP events around the standalone activation launches and the AMPBlock1 conv launches
-    (itts_amp_conv_fwd, C = 24 / 48 / 96, conv-only or with the activation fused), with their
-    algorithmic HBM bytes: valid rows x channels, each element read once and written once
-    (+ residual rows read; + the packed weights once)."""
-    orig_act, orig_amp = voc._act, voc._amp
+def install_hbm_timers(voc, t_act, t_amp, t_ampact=None):
+    """HIP events around the standalone activation launches, the AMPBlock1 conv launches
+    (itts_amp_conv_fwd, C = 24 / 48 / 96, conv-only or with the activation fused) and the fused
+    conv1 -> act2 launches (itts_amp_conv_act_fwd, C = 24 / 48), with their algorithmic HBM bytes: valid
+    rows x channels, each element read once and written once (+ residual rows read; + the packed
+    weights once)."""
+    orig_act, orig_amp, orig_ampact = voc._act, voc._amp, voc._amp_act
 
     def act(a, x, y, lens):
         nbytes = 2.0 * voc.rows * x.shape[2] * 2
@@ -103,7 +105,13 @@ def install_hbm_timers(voc, t_act, t_amp):
         return t_amp.wrap(lambda: orig_amp(c, x, y, lens, a, r1, r2, alpha), 2.0 * voc.rows * c.cout * c.cin * c.ntaps,
                           nbytes)
 
-    voc._act, voc._amp = act, amp
+    def amp_act(c, x, y, lens, a):
+        nbytes = 2.0 * voc.rows * (c.cin + c.cout) + 2.0 * c.ntaps * c.cin * c.cout
+        if t_ampact is None:
+            return orig_ampact(c, x, y, lens, a)
+        return t_ampact.wrap(lambda: orig_ampact(c, x, y, lens, a), 2.0 * voc.rows * c.cout * c.cin * c.ntaps, nbytes)
+
+    voc._act, voc._amp, voc._amp_act = act, amp, amp_act
 
 
 def _traffic(name, key):
@@ -265,9 +273,9 @@ def main():
         args.batch = 1
     B, N, L = args.batch, args.codes, args.text_len
     tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + L + 2 + 1 + N + 8)
-    timer, t_act, t_amp = KernelTimer(), KernelTimer(), KernelTimer()
+    timer, t_act, t_amp, t_ampact = KernelTimer(), KernelTimer(), KernelTimer(), KernelTimer()
     install_conv_timer(tts.vocoder, timer)
-    install_hbm_timers(tts.vocoder, t_act, t_amp)
+    install_hbm_timers(tts.vocoder, t_act, t_amp, t_ampact)
     # global batch of B * world utterances; utterance i runs on rank i % world (weak scaling)
     mels, texts = make_inputs(cfg, shard(B * world, world, rank), L, args.prompt_frames)
     mels = [m.to(dev) for m in mels]
@@ -290,6 +298,8 @@ def main():
         dist.barrier()
     if not args.no_kernel_timing:
         tts.gpt.step_events = []  # HIP events around every decode-step graph replay
+        if args.decoding == "beam3":  # distinct K/V rows per beam step (shared lineage counted once)
+            tts.gpt.beam_lineage = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     audio = 0.0
@@ -308,15 +318,16 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     step_ev, tts.gpt.step_events = tts.gpt.step_events, None
+    tts.gpt.beam_lineage = None
     if not args.no_kernel_timing:
         # the vocoder runs as ONE C-ABI call (itts_bigvgan_forward) in the timed steps; its implicit-GEMM
         # launches are timed one by one in an extra, untimed step through the Python launch sequence
         # (the same kernels, HipBigVGAN._forward_py)
         tts.vocoder.cforward = False
-        timer.enabled = t_act.enabled = t_amp.enabled = True
+        timer.enabled = t_act.enabled = t_amp.enabled = t_ampact.enabled = True
         step()
         torch.cuda.synchronize()
-        timer.enabled = t_act.enabled = t_amp.enabled = False
+        timer.enabled = t_act.enabled = t_amp.enabled = t_ampact.enabled = False
         tts.vocoder.cforward = True
     k_ms, k_flops, k_n = timer.result()
     dec = None
@@ -328,8 +339,8 @@ def main():
         pl = bool(tts.gpt.pl and tts.gpt._pl_ok({"B": rows}))
         body = ("20 x ONE persistent launch per layer (gpt_layer.hip: c_attn (ln_1 folded) -> attention -> "
                 "attn.c_proj split-K 8 + reduce -> c_fc (ln_2 folded, gelu) -> mlp.c_proj split-K 8 + reduce as "
-                "phases joined by in-launch hand-offs, weights prefetched by LDS-DMA) + counter reset kernel + "
-                "last-layer reduce/ln_f/final_norm" if pl else
+                "phases joined by in-launch hand-offs (epoch-tagged, nothing reset per step), weights prefetched "
+                "by LDS-DMA) + last-layer reduce/ln_f/final_norm" if pl else
                 "20 x [c_attn GEMM (ln_1 folded), attention, attn.c_proj GEMM split-K 8, reduce, c_fc GEMM "
                 "(ln_2 folded, gelu), mlp.c_proj GEMM (split-K 8), reduce]")
         dec = {"kernel": f"GPT decode step, {rows} rows (hipGraph: {body} + mel_head GEMM + " +
@@ -337,6 +348,10 @@ def main():
                "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
                "traffic": None, "launches": len(step_ev), "avg_launch_us": round(1e3 * d_ms / len(step_ev), 2),
                "algorithmic_bytes_per_launch": round(d_bytes / len(step_ev)), "share_of_step": round(d_ms / (1e3 * dt), 3)}
+        if args.decoding == "beam3":
+            dec["algorithmic_bytes_note"] = ("weights + distinct K/V rows per step: each utterance's prompt once, "
+                                             "generated positions once per distinct cache row among its beams "
+                                             "(lineage table at each replay's end), the step's new keys")
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -359,7 +374,9 @@ def main():
     for key, t, name, tkey in (("roofline_vocoder_act", t_act, "itts_aa_snakebeta_fwd (Activation1d, every AMP "
                                 "stage and activation_post)", "aa_snakebeta_bytes_per_launch"),
                                ("roofline_vocoder_amp", t_amp, "itts_amp_conv_fwd (AMPBlock1 dilated convs "
-                                "+ residuals, C = 24 / 48 / 96)", "amp_conv_bytes_per_launch")):
+                                "+ residuals, C = 24 / 48 / 96)", "amp_conv_bytes_per_launch"),
+                               ("roofline_vocoder_amp_act", t_ampact, "itts_amp_conv_act_fwd (AMPBlock1 conv1 -> "
+                                "act2 in one launch, C = 24 / 48)", "amp_conv_act_bytes_per_launch")):
         ms, _, n = t.result()
         if n:
             gbs = t.bytes / (ms * 1e-3) / 1e9
@@ -369,8 +386,9 @@ def main():
                         "algorithmic_bytes_per_launch": round(t.bytes / n),
                         "share_of_step": round(ms / (1e3 * dt / args.steps), 3)}
     if dec is not None:  # the decode step: the dominant unit of work
-        dec["traffic"] = _traffic(TRAFFIC_DECODE[(args.decoding, pl)], "bytes_per_step")
-        dec["traffic_source"] = f"profiles/{TRAFFIC_DECODE[(args.decoding, pl)]}"
+        tf = TRAFFIC_DECODE.get((args.decoding, pl))
+        dec["traffic"] = None if tf is None else _traffic(tf, "bytes_per_step")
+        dec["traffic_source"] = None if tf is None else f"profiles/{tf}"
     cpu = None
     if args.breakdown:
         ph = {}

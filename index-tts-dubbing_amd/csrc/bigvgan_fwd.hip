@@ -127,6 +127,10 @@ extern "C" int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* lat
                              a ? a->log_alpha : nullptr, a ? a->log_beta : nullptr, c.w, c.bias, r1, r2, y,
                              (int64_t)Tx * c.cout, c.cout, ln, B, Tx, c.cin, c.cout, c.ntaps, c.tap_off, alpha, stream);
   };
+  auto amp_act = [&](const ItTsConv& c, const uint16_t* x, int Tx, uint16_t* y, const int32_t* ln, const ItTsAct& a) {
+    return itts_amp_conv_act_fwd(x, (int64_t)Tx * c.cin, c.cin, c.w, c.bias, y, (int64_t)Tx * c.cout, c.cout, ln, B, Tx,
+                                 c.cin, c.cout, c.ntaps, c.tap_off, a.up12, a.down12, a.log_alpha, a.log_beta, stream);
+  };
   auto act = [&](const ItTsAct& a, const uint16_t* x, uint16_t* y, int C, int Tx, const int32_t* ln) {
     return itts_aa_snakebeta_fwd(x, y, a.up12, a.down12, a.log_alpha, a.log_beta, ln, B, C, Tx, (int64_t)Tx * C, C, 1,
                                  (int64_t)Tx * C, C, 1, ITTS_BF16, ITTS_BF16, stream);
@@ -158,6 +162,10 @@ extern "C" int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* lat
         if (st.amp_mode == 1) {  // activation fused into the conv's input staging
           rc = amp(ly.c1, src, Tn, t2, ln, &ly.a1, nullptr, nullptr, 1.0f);
           if (!rc) rc = amp(ly.c2, t2, Tn, dst, ln, &ly.a2, src, r2, alpha);
+        } else if (st.amp_mode == 3) {  // act kernel, conv1 with act2 in its epilogue, conv2 (+ residuals)
+          rc = act(ly.a1, src, t1, C, Tn, ln);
+          if (!rc) rc = amp_act(ly.c1, t1, Tn, t2, ln, ly.a2);
+          if (!rc) rc = amp(ly.c2, t2, Tn, dst, ln, nullptr, src, r2, alpha);
         } else if (st.amp_mode == 2) {  // activation kernel + the conv kernel without activation
           rc = act(ly.a1, src, t1, C, Tn, ln);
           if (!rc) rc = amp(ly.c1, t1, Tn, t2, ln, nullptr, nullptr, nullptr, 1.0f);

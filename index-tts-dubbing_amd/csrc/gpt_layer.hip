@@ -45,6 +45,8 @@
 // tag, a counter line some cache kept) is below / unequal to this launch's and can never satisfy a
 // poll, whatever happened between the launches (round 4 zeroed them per step: as a memset node that let
 // 30 of 64 reused-lane cues decode wrong data).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -58,6 +60,16 @@ constexpr int kQC = 12;                               // c_attn columns per work
 #define ITTS_PL_KB 4  // 8: 666.5 us per C3 step, 4: 661.3, 12: 684 (profiles/lib_ab2.sh)
 #endif
 constexpr int kKB = ITTS_PL_KB;  // attention keys per group per round (load depth; results do not depend on it)
+// steps of at most kSmallRows rows: each active (row, head) unit is alone on its CU and its key stream is
+// latency-bound (kKB keys per group = 32 KiB in flight per round): kKBSmall keys per group per round
+#ifndef ITTS_PL_KB_SMALL
+#define ITTS_PL_KB_SMALL 12
+#endif
+#ifndef ITTS_PL_SMALL_ROWS
+#define ITTS_PL_SMALL_ROWS 4
+#endif
+constexpr int kKBSmall = ITTS_PL_KB_SMALL, kSmallRows = ITTS_PL_SMALL_ROWS;
+static_assert(kKB % 4 == 0 && kKBSmall % 4 == 0, "keys per round: whole kSub chunks");
 constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
 constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s), then the grid drains
 // ITTS_PL_TRACE=1 (timing builds): wave 0 of every workgroup stamps the 100-MHz real-time counter at
@@ -206,8 +218,12 @@ __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uin
   }
 }
 
-template <int MT, bool ROWS>
+// WKEEP: this layer's weights read with the default cache policy instead of non-temporal, so that they can
+// stay in the 256-MiB Infinity Cache from one decode step to the next (the whole step streams 520 MB of
+// weights + the K/V, all non-temporal otherwise; ITTS_PL_KEEP_LAYERS picks how many layers)
+template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false>
 __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
+  constexpr int WAUX = WKEEP ? 0 : 2;  // LDS-DMA cache policy of the weight stream
   __shared__ __attribute__((aligned(16))) unsigned char lds_wo[8 * 1024];
   __shared__ __attribute__((aligned(16))) unsigned char lds_wfc[32 * 1024];
   __shared__ __attribute__((aligned(16))) unsigned char lds_wpj[32 * 1024];
@@ -221,8 +237,6 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   uint32_t* cnt = reinterpret_cast<uint32_t*>(p.scratch + kOffCnt);
   uint32_t* err = reinterpret_cast<uint32_t*>(p.scratch + kOffErr);
   uint32_t* seq = reinterpret_cast<uint32_t*>(p.scratch + kOffSeq);
-  // this launch's epoch (first needed at the end of phase A: the load's latency hides behind the operands)
-  const uint32_t L1 = ld_relaxed(seq) + 1u;
   // (no err check here: it cost a memory round trip before the first load; every poll and granule sweep
   // checks err every 256 spins, so after a timeout the grid still drains within one spin round per phase)
   uint64_t* gq = reinterpret_cast<uint64_t*>(p.scratch + kOffGq);
@@ -256,11 +270,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   const int w = wave;
   const int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
   const int kidx = p.kv_base + p.tstate[0] + p.kstep;
+  // this launch's epoch: a plain load (written by an earlier launch) beside the step counter's, so both are
+  // waited for together before the K/V addresses (an sc1 load at launch start was waited for on its own:
+  // +12 us per step, r05a)
+  const uint32_t L1 = *seq + 1u;
   // attention: this workgroup's rows of head h are 32 pt + 2 jj + u (pass pt, unit u = waves 4u .. 4u+3)
   const int u = w >> 2;
   const int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
   constexpr int NG = 32;
-  u32x4_t kr[kKB], vr[kKB];
+  u32x4_t kr[KB], vr[KB];
   // K/V rows of key index jk (0-based from the row's first valid key) of row `row`: the row's own cache
   // row, or (beams) the row of kv_rows[row][position] that holds that prefix position
   auto kv_ptr = [&](const uint16_t* cache, int row, int pos) -> const uint16_t* {
@@ -268,9 +286,9 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     if constexpr (ROWS) crow = p.kv_rows[(int64_t)row * p.ld_rows + pos];
     return cache + (int64_t)crow * p.cache_bs + (int64_t)h * p.cache_hs + (int64_t)pos * kHD + 8 * d8;
   };
-  auto kv_load = [&](u32x4_t (&dst)[kKB], const uint16_t* cache, int row, int p0, int nk, int j0) {
+  auto kv_load = [&](u32x4_t (&dst)[KB], const uint16_t* cache, int row, int p0, int nk, int j0) {
 #pragma unroll
-    for (int uu = 0; uu < kKB; ++uu) {
+    for (int uu = 0; uu < KB; ++uu) {
       const int jk = min(j0 + NG * uu + g, max(nk - 2, 0));
       dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk)));
     }
@@ -296,13 +314,13 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       // t is wave-uniform per m (w + 8 m): each branch is one uniform DMA into its own LDS object
       if (t < 8)
         __builtin_amdgcn_global_load_lds(p.o_w + (((int64_t)j * 64 + 8 * c + t) * 64 + lane),
-                                         (lds_void*)(lds_wo + t * 1024), 16, 0, 2);
+                                         (lds_void*)(lds_wo + t * 1024), 16, 0, WAUX);
       else if (t < 40)
         __builtin_amdgcn_global_load_lds(p.fc_w16 + (((int64_t)(32 * c + j) * 32 + (t - 8)) * 64 + lane),
-                                         (lds_void*)(lds_wfc + (t - 8) * 1024), 16, 0, 2);
+                                         (lds_void*)(lds_wfc + (t - 8) * 1024), 16, 0, WAUX);
       else
         __builtin_amdgcn_global_load_lds(p.proj_w + (((int64_t)j * 256 + 32 * c + (t - 40)) * 64 + lane),
-                                         (lds_void*)(lds_wpj + (t - 40) * 1024), 16, 0, 2);
+                                         (lds_void*)(lds_wpj + (t - 40) * 1024), 16, 0, WAUX);
     }
   };
   {
@@ -310,7 +328,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s = w + 8 * i;
-      bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
+      if constexpr (WKEEP)
+        bw[i] = wq[(s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0)];
+      else
+        bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
 #pragma unroll
       for (int t = 0; t < 2; ++t)
         av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
@@ -511,14 +532,14 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           xv[2 * i + 1] = __uint_as_float(r[i] & 0xFFFF0000u);
         }
       };
-      // one round of kKB keys per group; round 0 is peeled out of the loop: in straight-line code the
+      // one round of KB keys per group; round 0 is peeled out of the loop: in straight-line code the
       // compiler waits only for this round's K/V rows (issued at launch start), whereas a loop header
       // waits for every load in flight -- here also the weight DMA issued after the q/k/v sweep
       auto key_round = [&](int j0) __attribute__((always_inline)) {
-        const bool more = j0 + NG * kKB < nk;
-        float sc[kKB];
+        const bool more = j0 + NG * KB < nk;
+        float sc[KB];
 #pragma unroll
-        for (int uu = 0; uu < kKB; ++uu) {
+        for (int uu = 0; uu < KB; ++uu) {
           const int jk = j0 + NG * uu + g;
           float kx[8];
           unpack(kr[uu], kx);
@@ -532,9 +553,9 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           pt_ = sum8_dpp(pt_);
           sc[uu] = jk < nk ? pt_ : -INFINITY;
         }
-        if (more) kv_load(kr, p.kc, rr, p0, nk, j0 + NG * kKB);
+        if (more) kv_load(kr, p.kc, rr, p0, nk, j0 + NG * KB);
 #pragma unroll
-        for (int c0 = 0; c0 < kKB; c0 += kSub) {
+        for (int c0 = 0; c0 < KB; c0 += kSub) {
           float bm = -INFINITY;
 #pragma unroll
           for (int uu = c0; uu < c0 + kSub; ++uu) bm = fmaxf(bm, sc[uu]);
@@ -560,10 +581,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           }
           m_run = mn;
         }
-        if (more) kv_load(vr, p.vc, rr, p0, nk, j0 + NG * kKB);
+        if (more) kv_load(vr, p.vc, rr, p0, nk, j0 + NG * KB);
       };
       key_round(0);  // nk >= 1: round 0 always runs
-      for (int j0 = NG * kKB; j0 < nk; j0 += NG * kKB) key_round(j0);
+      for (int j0 = NG * KB; j0 < nk; j0 += NG * KB) key_round(j0);
       if (pt == 0) mark(20);
 #pragma unroll
       for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
@@ -855,6 +876,14 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 }
 
 int g_cu_count = -1;
+// layers 0 .. n-1 read their weights with the default cache policy (WKEEP); ITTS_PL_KEEP_LAYERS, default 0
+int keep_layers() {
+  static const int n = [] {
+    const char* e = getenv("ITTS_PL_KEEP_LAYERS");
+    return e ? atoi(e) : 0;
+  }();
+  return n;
+}
 
 }  // namespace
 
@@ -871,7 +900,8 @@ extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
     const void* ks[] = {reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, true>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, false>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, true>)};
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, true>),
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall>)};
     for (const void* k : ks) {
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess || nb < 1) occ = 0;
@@ -951,6 +981,18 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   (void)fnp;
   const int ki = 2 * (mt - 1) + (st->kv_rows ? 1 : 0);
   hipStream_t s = itts::as_stream(stream);
+  const bool keep = layer < keep_layers();
+  if (ki == 0 && st->rows <= kSmallRows) {
+    if (keep)
+      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, true>), dim3(kWG), dim3(kThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall>), dim3(kWG), dim3(kThreads), 0, s, a);
+    return itts::check_launch(fn);
+  }
+  if (ki == 0 && keep) {
+    hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKB, true>), dim3(kWG), dim3(kThreads), 0, s, a);
+    return itts::check_launch(fn);
+  }
   switch (ki) {
     case 0: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
     case 1: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;

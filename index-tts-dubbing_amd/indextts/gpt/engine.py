@@ -210,6 +210,9 @@ class HipGPT:
         self._pl_ran = False   # the last generate ran persistent layers (their error word is checked after it)
         self._lanes = {}  # lane index -> decode state, captured graph, stream
         self.step_events = None  # set to a list to time every decode step with HIP events (bench.py)
+        # beams + step_events: the kv_rows lineage table is snapshotted after every replay, and each step's
+        # key count becomes the DISTINCT (cache row, position) pairs its beams read (bench.py roofline)
+        self.beam_lineage = None
         self.logits_trace = None  # set to a list to record every step's raw logits [B, V] (tests)
         # algorithmic HBM bytes of one decode step: every weight byte once (+ per-key KV bytes)
         eb = 2 if dtype == "bf16" else 4
@@ -1127,13 +1130,37 @@ class HipGPT:
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
+                if self.beam_lineage is not None:  # after the event: not inside the timed interval
+                    self.beam_lineage.append((len(ev), steps, n, st["kv_rows"].clone()))
                 for j in range(n):
                     ev.append((e0 if j == 0 else e1, e1, R, keys0 + R * (steps + j)))
             prev = steps
             steps += n
             if steps // check_every != prev // check_every and bool(st["done_u"].all()):
                 break
+        if ev is not None and self.beam_lineage is not None:
+            self._beam_distinct_keys(ev, self.beam_lineage, B, K, s + 1, keys0)
+            self.beam_lineage = []
         return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
+
+    @staticmethod
+    def _beam_distinct_keys(ev, lineage, B, K, kv_base, keys0):
+        """Rewrite each beam step's key count (ev[i][3]) as the distinct K/V rows it reads: every utterance's
+        prompt once, the generated positions once per DISTINCT cache row among its beams' lineages (from the
+        lineage table at the end of the step's replay), and this step's new key of every row."""
+        R = B * K
+        for i0, step0, n, snap in lineage:
+            kv = snap.view(B, K, -1)
+            for j in range(n):
+                t = step0 + j  # this step writes position kv_base + t - 1 of every row
+                gen = kv[:, :, kv_base: kv_base + t - 1]
+                if gen.shape[2] > 0:
+                    srt = gen.sort(dim=1).values
+                    distinct = int(gen.shape[0] * gen.shape[2] + (srt[:, 1:] != srt[:, :-1]).sum())
+                else:
+                    distinct = 0
+                e0, e1, rows, _ = ev[i0 + j]
+                ev[i0 + j] = (e0, e1, rows, keys0 + distinct + R)
 
     def _beam_finalize(self, st, B, K, steps, max_new, length_penalty):
         """BeamSearchScorer.finalize: open beams of unfinished utterances become hypotheses (generated

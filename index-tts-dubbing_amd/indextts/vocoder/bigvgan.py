@@ -140,6 +140,11 @@ class HipBigVGAN:
     # act (vocoder 101 ms; act fused into the conv for 24 / 48: 107 ms);  others: act + igemm
     FUSED_CHANNELS = ()
     SPLIT_CHANNELS = (24, 48, 96)
+    # round 5: conv1 -> act2 of every layer in one launch (itts_amp_conv_act_fwd: the conv output's HBM round
+    # trip gone, bit-identical); ITTS_VOC_EPI="" turns it off (A/B)
+    EPI_CHANNELS = (24, 48)
+    if os.environ.get("ITTS_VOC_EPI") is not None:
+        EPI_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_EPI"].split(",") if v)
     if os.environ.get("ITTS_VOC_FUSED") is not None:  # tuning sweeps: "24,48,96"
         FUSED_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_FUSED"].split(",") if v)
         SPLIT_CHANNELS = tuple(sorted({24, 48, 96} - set(FUSED_CHANNELS)))
@@ -225,7 +230,7 @@ class HipBigVGAN:
         if self.fused_amp and C in self.FUSED_CHANNELS:
             return 1
         if self.fused_amp and C in self.SPLIT_CHANNELS:
-            return 2
+            return 3 if C in self.EPI_CHANNELS else 2
         return 0
 
     def _c_weights(self):
@@ -319,6 +324,14 @@ class HipBigVGAN:
             y.data_ptr(), Ty * y.shape[2], y.shape[2], lens.data_ptr(), B, T, Cin, c.cout, c.ntaps, c.offs,
             float(alpha), _hip.stream_ptr()), "itts_amp_conv_fwd")
 
+    def _amp_act(self, c: _Conv, x, y, lens, a: _Act):
+        """y = act(conv(x) + bias) in one launch (itts_amp_conv_act_fwd): conv1 -> act2 of a layer."""
+        B, T, Cin = x.shape
+        _hip.check(self.lib.itts_amp_conv_act_fwd(
+            x.data_ptr(), T * Cin, Cin, c.w.data_ptr(), c.bias.data_ptr(), y.data_ptr(), y.shape[1] * y.shape[2],
+            y.shape[2], lens.data_ptr(), B, T, Cin, c.cout, c.ntaps, c.offs, a.up.data_ptr(), a.down.data_ptr(),
+            a.alpha.data_ptr(), a.beta.data_ptr(), _hip.stream_ptr()), "itts_amp_conv_act_fwd")
+
     def _conv(self, c: _Conv, x, y, lens, r1=None, r2=None, alpha=1.0, bias_b=None, ymul=1, yoff=0, Tq=None):
         B, T, Cin = x.shape
         Ty = y.shape[1]
@@ -403,6 +416,10 @@ class HipBigVGAN:
                     if fused:  # activation fused into each conv's input staging (amp_conv.hip)
                         self._amp(c1, src, t2, lens_n, a1)
                         self._amp(c2, t2, dst, lens_n, a2, r1=src, r2=r2, alpha=alpha)
+                    elif split and C in self.EPI_CHANNELS:  # act kernel, conv1 -> act2 in one launch, conv2
+                        self._act(a1, src, t1, lens_n)
+                        self._amp_act(c1, t1, t2, lens_n, a2)
+                        self._amp(c2, t2, dst, lens_n, r1=src, r2=r2, alpha=alpha)
                     elif split:  # activation kernel + the all-channels conv kernel without activation
                         self._act(a1, src, t1, lens_n)
                         self._amp(c1, t1, t2, lens_n)

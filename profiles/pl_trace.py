@@ -26,7 +26,7 @@ def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
         del eng._lanes[k]
     eng.generate(conds, text, steps, min_new_tokens=steps)
     torch.cuda.synchronize()
-    OFF_TRACE = int(eng.lib.itts_gpt_pl_scratch_bytes()) - 256 - 256 * 32 * 8
+    OFF_TRACE = int(eng.lib.itts_gpt_pl_scratch_bytes()) - 512 - 256 * 32 * 8  # trace, epoch, error blocks
     tr = eng._pl_scratch.view(torch.uint8)[OFF_TRACE:OFF_TRACE + 256 * 32 * 8].view(torch.int64).view(256, 32)
     tr = tr[:, :21].cpu().double()
     t0 = tr[:, 0].min()

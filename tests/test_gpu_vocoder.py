@@ -448,3 +448,43 @@ def test_convtranspose_phases_as_output_columns_matches_torch(ci, co, k, u):
         err = (y[b, :L * u].cpu() - ref).abs()
         assert bool((err <= 1e-4 * scale + 1e-5).all()), float(err.max())
         assert bool((y[b, L * u:] == 9.0).all())
+
+
+@pytest.mark.parametrize("C,k,d,T,lens", [(24, 11, 5, 700, [700, 225, 224, 5, 1, 11]),
+                                          (24, 3, 1, 450, [450, 224, 231, 7, 2]),
+                                          (48, 7, 3, 700, [700, 448, 449, 3, 230]),
+                                          (48, 11, 1, 300, [300, 13, 6, 224])])
+def test_amp_conv_act_epilogue_equals_conv_then_activation(C, k, d, T, lens):
+    """itts_amp_conv_act_fwd (conv1 -> act2 of an AMPBlock1 layer in one launch, the activation run on the conv
+    tile in LDS) is BIT-identical to itts_amp_conv_fwd (no residuals, alpha 1) followed by the activation
+    kernel on its bf16 output: ragged lengths around the 224-row tile edges, utterances shorter than the
+    activation's 3-sample edge zones, every BigVGAN narrow-stage kernel size / dilation."""
+    from indextts.utils.synthetic import kaiser_sinc_lowpass
+    from indextts.vocoder.bigvgan import _Conv, conv1d_taps
+    _hip, lib = _lib()
+    torch.manual_seed(C * k + d + T)
+    B = len(lens)
+    lens_t = torch.tensor(lens, dtype=torch.int32).cuda()
+    x = torch.randn(B, T, C).to(torch.bfloat16).cuda()
+    conv = _Conv(*conv1d_taps(torch.randn(C, C, k) / (C * k) ** 0.5, d), torch.randn(C) * 0.1, C, C, "cuda")
+    up = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).float().cuda()
+    down = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).float().cuda() * 1.01
+    la, lb = (torch.randn(C) * 0.3).cuda(), (torch.randn(C) * 0.3).cuda()
+    s = _hip.stream_ptr()
+    t2 = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
+    want = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
+    _hip.check(lib.itts_amp_conv_fwd(x.data_ptr(), T * C, C, None, None, None, None, conv.w.data_ptr(),
+                                     conv.bias.data_ptr(), None, None, t2.data_ptr(), T * C, C, lens_t.data_ptr(), B, T,
+                                     C, C, conv.ntaps, conv.offs, 1.0, s), "amp_conv")
+    _hip.check(lib.itts_aa_snakebeta_fwd(t2.data_ptr(), want.data_ptr(), up.data_ptr(), down.data_ptr(), la.data_ptr(),
+                                         lb.data_ptr(), lens_t.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1,
+                                         _hip.BF16, _hip.BF16, s), "act")
+    got = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
+    _hip.check(lib.itts_amp_conv_act_fwd(x.data_ptr(), T * C, C, conv.w.data_ptr(), conv.bias.data_ptr(), got.data_ptr(),
+                                         T * C, C, lens_t.data_ptr(), B, T, C, C, conv.ntaps, conv.offs, up.data_ptr(),
+                                         down.data_ptr(), la.data_ptr(), lb.data_ptr(), s), "amp_conv_act")
+    torch.cuda.synchronize()
+    for b, L in enumerate(lens):
+        gb, wb = got[b, :L].view(torch.int16).cpu(), want[b, :L].view(torch.int16).cpu()
+        bad = (gb != wb).nonzero()
+        assert bad.numel() == 0, (b, L, bad[:8].tolist())
