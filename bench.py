@@ -318,6 +318,8 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     step_ev, tts.gpt.step_events = tts.gpt.step_events, None
+    if step_ev and tts.gpt.beam_lineage:  # beam3: distinct K/V rows per step, resolved after the timed region
+        tts.gpt.beam_distinct_keys(step_ev, tts.gpt.beam_lineage)
     tts.gpt.beam_lineage = None
     if not args.no_kernel_timing:
         # the vocoder runs as ONE C-ABI call (itts_bigvgan_forward) in the timed steps; its implicit-GEMM

@@ -255,7 +255,8 @@ __global__ __launch_bounds__(256, ITTS_ACT_WPS) void aa_snake_mfma_kernel(ActArg
 
     // ---- strips ----
     const int ts = t0 + sidx * 32 * S;  // first output of the strip
-    const int ntile = min(S, max(0, (len - ts + 31) / 32));
+    // NB = 3 (C = 96: whole 192-B rows per job): one strip per block, the fourth wave has none
+    const int ntile = sidx < NS ? min(S, max(0, (len - ts + 31) / 32)) : 0;
     itts_actm::strip<PX>(win, sidx * 32 * S, cb, ntile, T, a_rev, inv_b, [&](int i, const f32x16_t& acc) {
       const int t = ts + 32 * i + (lane & 31);
       if (t < 3 || t >= len - 3) return;  // edges: VALU fix-up below
@@ -284,6 +285,9 @@ __global__ __launch_bounds__(256, ITTS_ACT_WPS) void aa_snake_mfma_kernel(ActArg
   }
 }
 
+#ifndef ITTS_ACT_S  // 32-row output tiles per wave strip (job = (4 / NB) * 32 * S rows)
+#define ITTS_ACT_S 4
+#endif
 #ifndef ITTS_ACT_WGS  // resident workgroups targeted by the persistent activation grid
 #define ITTS_ACT_WGS 512
 #endif
@@ -320,6 +324,13 @@ void launch(const ActArgs& a, bool vec, bool vout, hipStream_t s) {
 }
 
 }  // namespace
+
+// C = 96 as ONE 3-block channel group per job (whole 192-B rows: every window row one contiguous read)
+// instead of three 1-block groups each reading 64 B of every row; ITTS_ACT_NB3=0: the 1-block form (A/B)
+bool act_nb3_enabled() {  // read per launch (tests toggle it in one process)
+  const char* e = getenv("ITTS_ACT_NB3");
+  return !(e && e[0] == '0');
+}
 
 // ITTS_ACT_MFMA=0 selects the VALU kernel for the bf16 channel-last layout too (A/B measurements)
 bool act_mfma_enabled() {
@@ -358,9 +369,10 @@ extern "C" int itts_aa_snakebeta_fwd(const void* x, void* y, const float* up12, 
   else if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16 && vec && vout && act_mfma_enabled()) {
     // the vocoder's layout: both FIRs on MFMA
     const int nblk = (C + 31) / 32;
-    if (nblk % 4 == 0) launch_mfma<4, 4>(a, s);
-    else if (nblk % 2 == 0) launch_mfma<2, 4>(a, s);
-    else launch_mfma<1, 4>(a, s);
+    if (nblk % 4 == 0) launch_mfma<4, ITTS_ACT_S>(a, s);
+    else if (nblk % 2 == 0) launch_mfma<2, ITTS_ACT_S>(a, s);
+    else if (nblk == 3 && act_nb3_enabled()) launch_mfma<3, 2 * ITTS_ACT_S>(a, s);
+    else launch_mfma<1, ITTS_ACT_S>(a, s);
   } else if (dtype_in == ITTS_BF16 && dtype_out == ITTS_BF16) launch<uint16_t, uint16_t>(a, vec, vout, s);
   else if (dtype_in == ITTS_F32 && dtype_out == ITTS_F32) launch<float, float>(a, false, false, s);
   else if (dtype_in == ITTS_F32) launch<float, uint16_t>(a, false, vout, s);

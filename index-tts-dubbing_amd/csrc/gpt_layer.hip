@@ -60,15 +60,22 @@ constexpr int kQC = 12;                               // c_attn columns per work
 #define ITTS_PL_KB 4  // 8: 666.5 us per C3 step, 4: 661.3, 12: 684 (profiles/lib_ab2.sh)
 #endif
 constexpr int kKB = ITTS_PL_KB;  // attention keys per group per round (load depth; results do not depend on it)
-// steps of at most kSmallRows rows: each active (row, head) unit is alone on its CU and its key stream is
-// latency-bound (kKB keys per group = 32 KiB in flight per round): kKBSmall keys per group per round
+// steps of at most kSmallRows rows (C2 = one row, the long-form tail chunks): the c_attn / c_fc phases skip the
+// second 16-row half of their A operands (H16) and the attention keeps kKBSmall keys per group per round in
+// flight.  C2 decode step (profiles/r05e_batch1.txt): 567-580 us with neither, 527-529 with H16 and 12 keys,
+// 521-523 with H16 and 8 (4: 524-525, 16: 545, which spills)
 #ifndef ITTS_PL_KB_SMALL
-#define ITTS_PL_KB_SMALL 12
+#define ITTS_PL_KB_SMALL 8
 #endif
 #ifndef ITTS_PL_SMALL_ROWS
-#define ITTS_PL_SMALL_ROWS 4
+#define ITTS_PL_SMALL_ROWS 16
 #endif
 constexpr int kKBSmall = ITTS_PL_KB_SMALL, kSmallRows = ITTS_PL_SMALL_ROWS;
+#ifndef ITTS_PL_SMALL_H16  // small steps also skip the second 16-row half of the c_attn / c_fc A operands
+#define ITTS_PL_SMALL_H16 1
+#endif
+constexpr bool kSmallH16 = ITTS_PL_SMALL_H16 != 0;
+static_assert(kSmallRows <= 16, "small steps fit one 16-row half");
 static_assert(kKB % 4 == 0 && kKBSmall % 4 == 0, "keys per round: whole kSub chunks");
 constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
 constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s), then the grid drains
@@ -221,9 +228,13 @@ __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uin
 // WKEEP: this layer's weights read with the default cache policy instead of non-temporal, so that they can
 // stay in the 256-MiB Infinity Cache from one decode step to the next (the whole step streams 520 MB of
 // weights + the K/V, all non-temporal otherwise; ITTS_PL_KEEP_LAYERS picks how many layers)
-template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false>
+// H16 (steps of at most 16 rows, MT = 1): the c_attn / c_fc phases load and multiply only the first 16-row
+// half of their A operands (rows 16-31 are padding: their outputs, never read, come out as the fold terms)
+template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false, bool H16 = false>
 __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
+  static_assert(!H16 || MT == 1, "16-row halves: one row tile");
   constexpr int WAUX = WKEEP ? 0 : 2;  // LDS-DMA cache policy of the weight stream
+  constexpr int NHF = H16 ? 1 : 2;     // 16-row halves of the A operands loaded / multiplied
   __shared__ __attribute__((aligned(16))) unsigned char lds_wo[8 * 1024];
   __shared__ __attribute__((aligned(16))) unsigned char lds_wfc[32 * 1024];
   __shared__ __attribute__((aligned(16))) unsigned char lds_wpj[32 * 1024];
@@ -333,7 +344,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       else
         bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NHF; ++t)
         av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -402,7 +413,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&bw[i]);
       const bf16x8_t bz = c16 < kQC ? bfr : bf16x8_t{};
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
+      for (int hf = 0; hf < NHF; ++hf) {
         const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&av[i][hf]);
         acc[hf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bz, acc[hf], 0, 0, 0);
 #pragma unroll
@@ -750,7 +761,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf)
+        for (int hf = 0; hf < NHF; ++hf)
           ax[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
               rsrc, ((c * kMaxR + 32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
       f32x4_t af[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
@@ -759,7 +770,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       for (int i = 0; i < 4; ++i) {
         const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(lds_wfc + (w + 8 * i) * 1024 + lane * 16);
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
+        for (int hf = 0; hf < NHF; ++hf) {
           const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&ax[i][hf]);
           af[hf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, af[hf], 0, 0, 0);
 #pragma unroll
@@ -876,11 +887,13 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 }
 
 int g_cu_count = -1;
-// layers 0 .. n-1 read their weights with the default cache policy (WKEEP); ITTS_PL_KEEP_LAYERS, default 0
+// layers 0 .. n-1 read their weights with the default cache policy (WKEEP), so ~100 MB of them can stay in the
+// Infinity Cache between steps: C3 decode step 657.7-657.9 us with none, 653.1-653.5 with 4, 652.7-654.4 with
+// 8, 663.8-664.0 with 12 (profiles/r05e_batch1.txt).  ITTS_PL_KEEP_LAYERS overrides (default 4)
 int keep_layers() {
   static const int n = [] {
     const char* e = getenv("ITTS_PL_KEEP_LAYERS");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 4;
   }();
   return n;
 }
@@ -901,7 +914,7 @@ extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, true>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, false>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, true>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall>)};
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>)};
     for (const void* k : ks) {
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess || nb < 1) occ = 0;
@@ -982,11 +995,12 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   const int ki = 2 * (mt - 1) + (st->kv_rows ? 1 : 0);
   hipStream_t s = itts::as_stream(stream);
   const bool keep = layer < keep_layers();
-  if (ki == 0 && st->rows <= kSmallRows) {
+  if (ki == 0 && st->rows <= kSmallRows) {  // kSmallRows <= 16: one 16-row half
     if (keep)
-      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, true>), dim3(kWG), dim3(kThreads), 0, s, a);
+      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, true, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s, a);
     else
-      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall>), dim3(kWG), dim3(kThreads), 0, s, a);
+      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s,
+                         a);
     return itts::check_launch(fn);
   }
   if (ki == 0 && keep) {

@@ -1138,16 +1138,27 @@ class HipGPT:
             steps += n
             if steps // check_every != prev // check_every and bool(st["done_u"].all()):
                 break
-        if ev is not None and self.beam_lineage is not None:
-            self._beam_distinct_keys(ev, self.beam_lineage, B, K, s + 1, keys0)
-            self.beam_lineage = []
+        if ev is not None and self.beam_lineage is not None:  # resolved by the caller, outside its timed region
+            self.beam_lineage.append(("shape", B, K, s + 1, keys0))
         return self._beam_finalize(st, B, K, steps, max_new_tokens, length_penalty)
 
     @staticmethod
-    def _beam_distinct_keys(ev, lineage, B, K, kv_base, keys0):
+    def beam_distinct_keys(ev, lineage):
         """Rewrite each beam step's key count (ev[i][3]) as the distinct K/V rows it reads: every utterance's
         prompt once, the generated positions once per DISTINCT cache row among its beams' lineages (from the
-        lineage table at the end of the step's replay), and this step's new key of every row."""
+        lineage table at the end of the step's replay), and this step's new key of every row.  ``lineage``:
+        what generate_beam recorded with ``beam_lineage`` set (snapshots, then a ("shape", ...) entry per call)."""
+        recs = []
+        for e in lineage:
+            if e[0] == "shape":
+                _, B, K, kv_base, keys0 = e
+                HipGPT._beam_distinct_keys_call(ev, recs, B, K, kv_base, keys0)
+                recs = []
+            else:
+                recs.append(e)
+
+    @staticmethod
+    def _beam_distinct_keys_call(ev, lineage, B, K, kv_base, keys0):
         R = B * K
         for i0, step0, n, snap in lineage:
             kv = snap.view(B, K, -1)

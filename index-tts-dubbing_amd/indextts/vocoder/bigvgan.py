@@ -140,9 +140,11 @@ class HipBigVGAN:
     # act (vocoder 101 ms; act fused into the conv for 24 / 48: 107 ms);  others: act + igemm
     FUSED_CHANNELS = ()
     SPLIT_CHANNELS = (24, 48, 96)
-    # round 5: conv1 -> act2 of every layer in one launch (itts_amp_conv_act_fwd: the conv output's HBM round
-    # trip gone, bit-identical); ITTS_VOC_EPI="" turns it off (A/B)
-    EPI_CHANNELS = (24, 48)
+    # round 5: conv1 -> act2 of a layer in one launch (itts_amp_conv_act_fwd: the conv output's HBM round trip
+    # gone, bit-identical).  Measured NOT faster (profiles/ubench_epi_r05.txt: C = 48 at parity, C = 24 up to
+    # 14 % slower than conv + activation kernel: the fused tile runs the activation's MFMA chains after the
+    # conv's at 3 waves per SIMD), so off by default; ITTS_VOC_EPI="24,48" turns it on (A/B)
+    EPI_CHANNELS = ()
     if os.environ.get("ITTS_VOC_EPI") is not None:
         EPI_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_EPI"].split(",") if v)
     if os.environ.get("ITTS_VOC_FUSED") is not None:  # tuning sweeps: "24,48,96"

@@ -108,7 +108,34 @@ def test_activation_kernel_bf16_mfma_path_vs_f32_path(C):
     assert float(same) > 0.6, float(same)
 
 
-@pytest.mark.parametrize("C,B,T", [(24, 160, 3000), (768, 64, 700), (192, 48, 1500)])
+def test_activation_kernel_c96_whole_row_jobs_equal_block_jobs(monkeypatch):
+    """C = 96 runs as ONE 3-block channel group per job (whole 192-B rows, ITTS_ACT_NB3=1, default) instead of
+    three 1-block groups: the same per-channel-block MFMA arithmetic over the same window rows, so the
+    outputs are bit-identical, ragged lengths included."""
+    from indextts.utils.synthetic import kaiser_sinc_lowpass
+    _hip, lib = _lib()
+    C, B, T = 96, 40, 2100
+    g = torch.Generator().manual_seed(C + B)
+    lens = torch.randint(1, T + 1, (B,), generator=g, dtype=torch.int32)
+    lens[0], lens[1], lens[2] = T, 1, 5
+    x = (torch.randn(B, T, C, generator=g) * 1.5).to(torch.bfloat16).cuda()
+    f = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).cuda()
+    la, lb = (torch.randn(C, generator=g) * 0.5).cuda(), (torch.randn(C, generator=g) * 0.5).cuda()
+    lensd = lens.cuda()
+    out = []
+    for nb3 in ("1", "0"):
+        monkeypatch.setenv("ITTS_ACT_NB3", nb3)
+        y = torch.full((B, T, C), -12352.0, dtype=torch.bfloat16, device="cuda")
+        _hip.check(lib.itts_aa_snakebeta_fwd(x.data_ptr(), y.data_ptr(), f.data_ptr(), f.data_ptr(), la.data_ptr(),
+                                             lb.data_ptr(), lensd.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1,
+                                             _hip.BF16, _hip.BF16, _hip.stream_ptr()), "fwd")
+        torch.cuda.synchronize()
+        out.append(y.view(torch.int16).cpu())
+    bad = (out[0] != out[1]).nonzero()
+    assert bad.numel() == 0, (bad[:8].tolist(), lens.tolist())
+
+
+@pytest.mark.parametrize("C,B,T", [(24, 160, 3000), (768, 64, 700), (192, 48, 1500), (96, 24, 2100)])
 def test_activation_kernel_mfma_persistent_many_jobs(C, B, T):
     """The MFMA activation kernel is persistent (each workgroup walks several (utterance, time tile)
     jobs with the next window's loads in flight): shapes with more jobs than resident workgroups and
