@@ -38,9 +38,11 @@ PEAK_HBM_GBS = 8000.0
 # PMC traffic summaries of the CURRENT build (profiles/run_profiles.sh; FETCH_SIZE x2 per
 # MI355X_MICROARCH.md, calibrated by profiles/pmc_calibrate.py); None when not yet measured
 # per decoding and decode path (persistent layers or the launch chain): None until measured for this build
-TRAFFIC_DECODE = {("greedy", True): "traffic_decode_pl_r04j.json", ("greedy", False): "traffic_decode_r04.json",
-                  ("beam3", False): "traffic_decode_beam3_r04h.json"}
-TRAFFIC_VOCODER = "traffic_vocoder_r03s.json"
+# PMC files are measured on the C3 workload (profiles/pmc_decode.py, pmc_vocoder.py): other workloads report
+# traffic null rather than C3's bytes
+TRAFFIC_DECODE = {("c3", "greedy", True): "traffic_decode_pl_r05f.json", ("c3", "greedy", False): "traffic_decode_r04.json",
+                  ("c3", "beam3", False): "traffic_decode_beam3_r05f.json"}
+TRAFFIC_VOCODER = {"c3": "traffic_vocoder_r05f.json"}
 
 
 class KernelTimer:
@@ -115,7 +117,9 @@ def install_hbm_timers(voc, t_act, t_amp, t_ampact=None):
 
 
 def _traffic(name, key):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/run_profiles.sh)."""
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/run_profiles_r05.sh)."""
+    if name is None:
+        return None
     path = os.path.join(REPO, "profiles", name)
     if not os.path.exists(path):
         return None
@@ -368,7 +372,7 @@ def main():
     voc = {"kernel": "itts_igemm_fwd (BigVGAN convs C >= 192 and ConvTranspose phases, MFMA bf16)", "bound": "mfma",
            "achieved": None if achieved is None else round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
            "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / PEAK_BF16_TFLOPS, 4),
-           "traffic": _traffic(TRAFFIC_VOCODER, "igemm_bytes_per_launch"), "launches": k_n,
+           "traffic": _traffic(TRAFFIC_VOCODER.get(args.workload), "igemm_bytes_per_launch"), "launches": k_n,
            "avg_launch_us": round(1e3 * k_ms / max(k_n, 1), 2),
            "algorithmic_bytes_per_launch": round(timer.bytes / max(k_n, 1)),
            "share_of_step": round(k_ms / (1e3 * dt / args.steps), 3)}
@@ -383,12 +387,12 @@ def main():
         if n:
             gbs = t.bytes / (ms * 1e-3) / 1e9
             hbm[key] = {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": _traffic(TRAFFIC_VOCODER, tkey),
+                        "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": _traffic(TRAFFIC_VOCODER.get(args.workload), tkey),
                         "launches": n, "avg_launch_us": round(1e3 * ms / n, 2),
                         "algorithmic_bytes_per_launch": round(t.bytes / n),
                         "share_of_step": round(ms / (1e3 * dt / args.steps), 3)}
     if dec is not None:  # the decode step: the dominant unit of work
-        tf = TRAFFIC_DECODE.get((args.decoding, pl))
+        tf = TRAFFIC_DECODE.get((args.workload, args.decoding, pl))
         dec["traffic"] = None if tf is None else _traffic(tf, "bytes_per_step")
         dec["traffic_source"] = None if tf is None else f"profiles/{tf}"
     cpu = None

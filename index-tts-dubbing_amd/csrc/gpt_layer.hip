@@ -71,6 +71,9 @@ constexpr int kKB = ITTS_PL_KB;  // attention keys per group per round (load dep
 #define ITTS_PL_SMALL_ROWS 16
 #endif
 constexpr int kKBSmall = ITTS_PL_KB_SMALL, kSmallRows = ITTS_PL_SMALL_ROWS;
+#ifndef ITTS_PL_DMA_SPLIT  // small steps: an idle unit's waves issue the weight DMA of a half-active workgroup
+#define ITTS_PL_DMA_SPLIT 1
+#endif
 #ifndef ITTS_PL_SMALL_H16  // small steps also skip the second 16-row half of the c_attn / c_fc A operands
 #define ITTS_PL_SMALL_H16 1
 #endif
@@ -318,11 +321,18 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   }
   // this workgroup's attn.c_proj (8 KiB), c_fc (32 KiB), mlp.c_proj (32 KiB) weight slices, global ->
   // LDS by DMA (1 KiB per wave instruction, lane-linear = fragment order, nt), instruction t by wave t % 8
+  // small steps (H16) in a workgroup whose unit 0 has a row and unit 1 none (odd R; C2: R = 1): unit 1's idle
+  // waves issue the whole burst, so unit 0's later K/V rounds do not retire behind it (in-order vmcnt) -- at
+  // one row per head those few units are the critical path
+  const bool dma_split = ITTS_PL_DMA_SPLIT && H16 && 2 * jj < R && 2 * jj + 1 >= R;  // workgroup-uniform
   auto issue_dma = [&]() {
+    if (dma_split && w < 4) return;
+    const int wd = dma_split ? w - 4 : w, nwd = dma_split ? 4 : 8;
 #pragma unroll
-    for (int m = 0; m < 9; ++m) {
-      const int t = w + 8 * m;
-      // t is wave-uniform per m (w + 8 m): each branch is one uniform DMA into its own LDS object
+    for (int m = 0; m < 18; ++m) {
+      const int t = wd + nwd * m;
+      if (t >= 72) break;
+      // t is wave-uniform per m: each branch is one uniform DMA into its own LDS object
       if (t < 8)
         __builtin_amdgcn_global_load_lds(p.o_w + (((int64_t)j * 64 + 8 * c + t) * 64 + lane),
                                          (lds_void*)(lds_wo + t * 1024), 16, 0, WAUX);
