@@ -71,6 +71,15 @@ constexpr int kKB = ITTS_PL_KB;  // attention keys per group per round (load dep
 #define ITTS_PL_SMALL_ROWS 16
 #endif
 constexpr int kKBSmall = ITTS_PL_KB_SMALL, kSmallRows = ITTS_PL_SMALL_ROWS;
+#ifndef ITTS_PL_KEEP_QKV  // every layer's c_attn operands with the default cache policy (A/B)
+#define ITTS_PL_KEEP_QKV 1
+#endif
+#ifndef ITTS_PL_DMA_LATE
+#define ITTS_PL_DMA_LATE 0
+#endif
+#ifndef ITTS_PL_KV_UNCOND
+#define ITTS_PL_KV_UNCOND 1
+#endif
 #ifndef ITTS_PL_DMA_SPLIT  // small steps: an idle unit's waves issue the weight DMA of a half-active workgroup
 #define ITTS_PL_DMA_SPLIT 1
 #endif
@@ -325,23 +334,29 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   // waves issue the whole burst, so unit 0's later K/V rounds do not retire behind it (in-order vmcnt) -- at
   // one row per head those few units are the critical path
   const bool dma_split = ITTS_PL_DMA_SPLIT && H16 && 2 * jj < R && 2 * jj + 1 >= R;  // workgroup-uniform
+  auto dma_one = [&](int t) {
+    // t is wave-uniform: each branch is one uniform DMA into its own LDS object
+    if (t < 8)
+      __builtin_amdgcn_global_load_lds(p.o_w + (((int64_t)j * 64 + 8 * c + t) * 64 + lane),
+                                       (lds_void*)(lds_wo + t * 1024), 16, 0, WAUX);
+    else if (t < 40)
+      __builtin_amdgcn_global_load_lds(p.fc_w16 + (((int64_t)(32 * c + j) * 32 + (t - 8)) * 64 + lane),
+                                       (lds_void*)(lds_wfc + (t - 8) * 1024), 16, 0, WAUX);
+    else
+      __builtin_amdgcn_global_load_lds(p.proj_w + (((int64_t)j * 256 + 32 * c + (t - 40)) * 64 + lane),
+                                       (lds_void*)(lds_wpj + (t - 40) * 1024), 16, 0, WAUX);
+  };
+  // straight-line issue (a data-dependent trip count leaves the compiler's vmcnt tracking a join it resolves
+  // with vmcnt(0): the first key round then waited for the whole burst)
   auto issue_dma = [&]() {
-    if (dma_split && w < 4) return;
-    const int wd = dma_split ? w - 4 : w, nwd = dma_split ? 4 : 8;
+    if (dma_split) {
+      if (w >= 4) {
 #pragma unroll
-    for (int m = 0; m < 18; ++m) {
-      const int t = wd + nwd * m;
-      if (t >= 72) break;
-      // t is wave-uniform per m: each branch is one uniform DMA into its own LDS object
-      if (t < 8)
-        __builtin_amdgcn_global_load_lds(p.o_w + (((int64_t)j * 64 + 8 * c + t) * 64 + lane),
-                                         (lds_void*)(lds_wo + t * 1024), 16, 0, WAUX);
-      else if (t < 40)
-        __builtin_amdgcn_global_load_lds(p.fc_w16 + (((int64_t)(32 * c + j) * 32 + (t - 8)) * 64 + lane),
-                                         (lds_void*)(lds_wfc + (t - 8) * 1024), 16, 0, WAUX);
-      else
-        __builtin_amdgcn_global_load_lds(p.proj_w + (((int64_t)j * 256 + 32 * c + (t - 40)) * 64 + lane),
-                                         (lds_void*)(lds_wpj + (t - 40) * 1024), 16, 0, WAUX);
+        for (int m = 0; m < 18; ++m) dma_one(w - 4 + 4 * m);
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < 9; ++m) dma_one(w + 8 * m);
     }
   };
   {
@@ -349,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s = w + 8 * i;
-      if constexpr (WKEEP)
+      if constexpr (WKEEP || ITTS_PL_KEEP_QKV)
         bw[i] = wq[(s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0)];
       else
         bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
@@ -535,7 +550,9 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     if (*abort_flag) return;
     // the later phases' weights: behind the c_attn operands and this pass's K/V rows, after the q/k/v
     // granule sweep (a burst issued earlier queued in front of those loads: profiles/pl_trace_r04b.txt)
-    if (!ITTS_PL_DMA_EARLY && pt == 0) issue_dma();
+    // ITTS_PL_DMA_LATE: the burst goes out after the first key round (its K/V rows, in flight since launch
+    // start, are then waited for on their own: behind an LDS-DMA the compiler can only emit vmcnt(0))
+    if (!ITTS_PL_DMA_EARLY && !ITTS_PL_DMA_LATE && pt == 0) issue_dma();
     if (act_u) {
       float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       float m_run = -INFINITY, l_run = 0.f;
@@ -557,7 +574,13 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       // compiler waits only for this round's K/V rows (issued at launch start), whereas a loop header
       // waits for every load in flight -- here also the weight DMA issued after the q/k/v sweep
       auto key_round = [&](int j0) __attribute__((always_inline)) {
-        const bool more = j0 + NG * KB < nk;
+        // ITTS_PL_KV_UNCOND (full steps): the next round's rows are requested whether or not it exists (past
+        // the last key every lane's index clamps to the row's key nk - 2), so the issue count is the same on
+        // every path and the compiler's waits stay counted -- a conditional issue merges into vmcnt(0), and
+        // this round's V rows were then waited for together with the next round's K rows: C3 step 648.8 /
+        // 649.5 -> 640.8 / 640.6 us.  Small steps keep the conditional issue: there the one active unit's
+        // useless last round sits on the critical path (C2 504.8 / 504.3 -> 516.7 / 517.3 us unconditional)
+        const bool more = (ITTS_PL_KV_UNCOND && !H16) || j0 + NG * KB < nk;
         float sc[KB];
 #pragma unroll
         for (int uu = 0; uu < KB; ++uu) {
@@ -605,6 +628,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         if (more) kv_load(vr, p.vc, rr, p0, nk, j0 + NG * KB);
       };
       key_round(0);  // nk >= 1: round 0 always runs
+      if (ITTS_PL_DMA_LATE && !ITTS_PL_DMA_EARLY && pt == 0) {
+        asm volatile("" ::: "memory");
+        issue_dma();
+      }
+      if (pt == 0) mark(21);
       for (int j0 = NG * KB; j0 < nk; j0 += NG * KB) key_round(j0);
       if (pt == 0) mark(20);
 #pragma unroll
@@ -613,6 +641,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         gm[g] = m_run;
         gl[g] = l_run;
       }
+    }
+    // (after the block, not as its else: the structurizer turns an else into a DMA block ahead of the
+    // attention, whose join then forces vmcnt(0) on the active units' first key round)
+    if (ITTS_PL_DMA_LATE && !ITTS_PL_DMA_EARLY && pt == 0) {
+      // an opaque copy of !act_u: with the plain condition the compiler turns this into the else of the
+      // attention block, laid out ahead of it, and the join makes the active units' first wait vmcnt(0)
+      int idle = !act_u;
+      asm volatile("" : "+v"(idle)::"memory");
+      if (idle) issue_dma();
     }
     bar();
     if (act_u) {
@@ -897,13 +934,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 }
 
 int g_cu_count = -1;
-// layers 0 .. n-1 read their weights with the default cache policy (WKEEP), so ~100 MB of them can stay in the
-// Infinity Cache between steps: C3 decode step 657.7-657.9 us with none, 653.1-653.5 with 4, 652.7-654.4 with
-// 8, 663.8-664.0 with 12 (profiles/r05e_batch1.txt).  ITTS_PL_KEEP_LAYERS overrides (default 4)
+// layers 0 .. n-1 read ALL their weights with the default cache policy (WKEEP), so they can stay in the Infinity
+// Cache between steps: C3 decode step 657.7-657.9 us with none, 653.1-653.5 with 4, 652.7-654.4 with 8,
+// 663.8-664.0 with 12 (profiles/r05e_batch1.txt).  Since every layer's c_attn operands are read that way
+// (ITTS_PL_KEEP_QKV: 126 MB, the launch head's critical path) none is best: 646.0-646.9 vs 646.1-649.9 with 4
+// (C2 505.9 vs 508.6-510.6).  ITTS_PL_KEEP_LAYERS overrides (default 0)
 int keep_layers() {
   static const int n = [] {
     const char* e = getenv("ITTS_PL_KEEP_LAYERS");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 0;
   }();
   return n;
 }

@@ -15,7 +15,8 @@ from indextts.utils.synthetic import gpt_state_dict  # noqa: E402
 
 NAMES = ["start", "A0 issued", "A c_attn", "E1 q/k/v in", "B attention", "E2 o ready", "C c_proj",
          "E3 part ready", "D x1", "E4 x1 ready", "E c_fc", "E5 f ready", "F mlp.c_proj", "E6 part ready",
-         "G end", "E2 drained", "E3 drained", "E4 drained", "E5 drained", "E6 drained", "B keys done"]
+         "G end", "E2 drained", "E3 drained", "E4 drained", "E5 drained", "E6 drained", "B keys done",
+         "B round 0 done"]
 
 
 def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
@@ -28,12 +29,14 @@ def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
     torch.cuda.synchronize()
     OFF_TRACE = int(eng.lib.itts_gpt_pl_scratch_bytes()) - 512 - 256 * 32 * 8  # trace, epoch, error blocks
     tr = eng._pl_scratch.view(torch.uint8)[OFF_TRACE:OFF_TRACE + 256 * 32 * 8].view(torch.int64).view(256, 32)
-    tr = tr[:, :21].cpu().double()
+    tr = tr[:, :22].cpu().double()
     t0 = tr[:, 0].min()
     rel = (tr - t0) / 100.0  # 100 MHz -> µs
+    os.makedirs("gpurun_out", exist_ok=True)
+    torch.save(rel.clone(), f"gpurun_out/pl_trace_raw_B{B}_{steps}.pt")
     print(f"B={B}, {steps} steps (keys at the traced step: {32 + L_text + 2 + steps}): layer span {float(rel[:, 14].max()):.2f} us (first start -> last end)")
     prev = None
-    order = [0, 1, 2, 3, 20, 4, 15, 5, 6, 16, 7, 8, 17, 9, 10, 18, 11, 12, 19, 13, 14]
+    order = [0, 1, 2, 3, 21, 20, 4, 15, 5, 6, 16, 7, 8, 17, 9, 10, 18, 11, 12, 19, 13, 14]
     for i in order:
         n = NAMES[i]
         col = rel[:, i]
@@ -43,6 +46,19 @@ def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
             line += f"   | per-WG dt med {float(d.median()):6.2f} max {float(d.max()):6.2f}"
         print(line, flush=True)
         prev = col
+    # hand-off protocol latency per edge: the last producer's add (after its drain) -> each consumer's poll
+    # match.  Cluster edges (E2, E4, E5): producers and consumers = the 32 workgroups b % 8 == c; tile edges
+    # (E3, E6): the 8 workgroups of tile j = b / 8
+    b = torch.arange(256)
+    for name, m_add, m_rdy, key in (("E2", 15, 5, b % 8), ("E3", 16, 7, b // 8), ("E4", 17, 9, b % 8),
+                                    ("E5", 18, 11, b % 8), ("E6", 19, 13, b // 8)):
+        lat = []
+        for k in key.unique():
+            sel = key == k
+            lat.append(rel[sel, m_rdy] - rel[sel, m_add].max())
+        lat = torch.cat(lat)
+        print(f"  {name}: last add -> ready  min {float(lat.min()):5.2f} med {float(lat.median()):5.2f} "
+              f"max {float(lat.max()):5.2f} us", flush=True)
 
 
 if __name__ == "__main__":
