@@ -142,7 +142,7 @@ constexpr int kMaxR = 128;
 #define ITTS_PL_CNT_STRIDE 1024
 #endif
 constexpr int kCntStride = ITTS_PL_CNT_STRIDE;  // u32 units
-constexpr int kNumCnt = 88;
+constexpr int kNumCnt = 152;
 constexpr int64_t kOffCnt = 0;
 constexpr int64_t kOffGq = ((int64_t)kNumCnt * kCntStride * 4 + 511) / 512 * 512;                                       // [128 rows][16 heads][192] u64
 constexpr int64_t kOffOb = kOffGq + (int64_t)kMaxR * kH * 192 * 8;    // [8][128][128] bf16
@@ -155,7 +155,11 @@ constexpr int64_t kOffSeq = kOffTrace + (int64_t)kWG * 32 * 8;        // u32 epo
 constexpr int64_t kOffErr = kOffSeq + 256;                             // sticky error word
 constexpr int64_t kScratchBytes = kOffErr + 256;
 constexpr int64_t kZeroBytes = kOffGq + (int64_t)kMaxR * kH * 192 * 8;  // counters + every granule (x16)
-enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56 };
+// CNT7: the layer seam inside a multi-layer launch (x^ of layer l -> c_attn of layer l + 1): 8 x 8 counters
+// [producer cluster][consumer cluster], each with the 32 adders of its producer cluster and the 32 pollers of its
+// consumer cluster (workgroup 8j + c adds to CNT7 + 8c + r for every r: one wave instruction, 8 lanes; polls
+// CNT7 + 8q + c for every q, 8 lanes).  One counter for all 256 adders serialised their atomics: ~1.3 us per seam.
+enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56, CNT7 = 88 };
 
 // LDS layout (bytes)
 constexpr int L_WO = 0, L_WFC = L_WO + 8 * 1024, L_WPJ = L_WFC + 32 * 1024, L_RED = L_WPJ + 32 * 1024;
@@ -172,7 +176,8 @@ constexpr int kRestBytes = kLdsBytes - L_RED;  // everything after the weight sl
 // scratch and put `s_waitcnt vmcnt(0)` (the whole 72 KiB DMA) in front of every LDS access after the
 // DMA issue; distinct objects get distinct alias scopes, so only the reads of the weights wait.
 
-struct PlArgs {
+// one layer's weights (kernel arguments: the launch's layers are indexed by the loop counter)
+struct PlLayerPtrs {
   const u32x4_t* qkv_w12;  // [256][32 ks][4 q][12 c] x 16 B
   const float* qkv_uc;     // [256][2][12]
   const u32x4_t* o_w;      // attn.c_proj, pack_skinny [32 tiles][64 ks][64][8]
@@ -181,18 +186,27 @@ struct PlArgs {
   const float *fc_u, *fc_c;
   const u32x4_t* proj_w;   // mlp.c_proj, pack_skinny [32 tiles][256 ks][64][8]
   const float* proj_b;
+};
+constexpr int kMaxLpl = 32;  // layers per launch (kernel-argument table; 32 x 72 B)
+struct PlCommon {
   float* x;                // [R][1024] f32
   uint16_t* xh;            // [32][1024] bf16 (rows >= R: read, never written)
-  uint16_t *kc, *vc;       // this layer's cache [R][16][max_kv][64]
-  int64_t cache_bs, cache_hs;
+  uint16_t *kc, *vc;       // layer `layer`'s cache [R][16][max_kv][64]; layer + i at + i * layer_cache
+  int64_t cache_bs, cache_hs, layer_cache;
   const int32_t* pad;
   const int32_t* tstate;
   const int32_t* kv_rows;  // beams: [R][ld_rows] cache row of each prefix position, else null
   int64_t ld_rows;
-  int kv_base, kstep, R, layer, last;
+  int kv_base, kstep, R, layer, nl, last;  // layers layer .. layer + nl - 1; last: the model's last among them
+  int seam;  // every layer adds to the CNT7 seam counters (a process that runs multi-layer launches)
   float eps;
   unsigned char* scratch;
 };
+template <int NLY>
+struct PlArgsT : PlCommon {
+  PlLayerPtrs ly[NLY];
+};
+// one-layer launches keep the round-4 argument size (~200 B); multi-layer launches carry the whole table
 
 // workgroup barrier that waits for this wave's LDS traffic only: a __syncthreads() would also drain
 // every vector-memory load in flight (the K/V rows requested ahead of the c_attn phase)
@@ -201,6 +215,8 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
+// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= n only (expcnt / lgkmcnt at their maxima)
+constexpr int vm_wait_enc(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 // every storing wave's write-through stores have left (Guideline 16 R1: before the counter add)
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -242,8 +258,9 @@ __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uin
 // weights + the K/V, all non-temporal otherwise; ITTS_PL_KEEP_LAYERS picks how many layers)
 // H16 (steps of at most 16 rows, MT = 1): the c_attn / c_fc phases load and multiply only the first 16-row
 // half of their A operands (rows 16-31 are padding: their outputs, never read, come out as the fold terms)
-template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false, bool H16 = false>
-__global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
+// MULTI: the launch runs p.nl layers joined by the seam; else one layer (p.nl == 1), straight-line code
+template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false, bool H16 = false, bool MULTI = false>
+__global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? kMaxLpl : 1> p) {
   static_assert(!H16 || MT == 1, "16-row halves: one row tile");
   constexpr int WAUX = WKEEP ? 0 : 2;  // LDS-DMA cache policy of the weight stream
   constexpr int NHF = H16 ? 1 : 2;     // 16-row halves of the A operands loaded / multiplied
@@ -253,21 +270,34 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds_rest[kRestBytes];
   unsigned char* const smem = lds_rest - L_RED;  // offsets >= L_RED address lds_rest
   typedef __attribute__((address_space(3))) void lds_void;
-  const int b = blockIdx.x, c = b % kNC, j = b / kNC;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int b = blockIdx.x;
+  int c = b % kNC, j = b / kNC;  // (MULTI: laundered per layer)
+  int zz = 0;  // MULTI: an opaque zero per layer (see the layer loop)
+  int tid = threadIdx.x, lane = tid & 63;  // (laundered per layer: see the layer loop)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hh = j >> 4, jj = j & 15, h = 2 * c + hh;
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(p.scratch + kOffCnt);
-  uint32_t* err = reinterpret_cast<uint32_t*>(p.scratch + kOffErr);
+  int hh = j >> 4, jj = j & 15, h = 2 * c + hh;
+  // scratch regions.  MULTI: every use takes a fresh opaque copy of the scratch base, so the compiler cannot keep
+  // the dozen derived pointers / buffer descriptors live across the whole layer loop (they spilled: 118 SGPRs to
+  // VGPR lanes, a readlane in every phase)
+  auto scr = [&]() __attribute__((always_inline)) {
+    unsigned char* q = p.scratch;
+    if constexpr (MULTI) asm volatile("" : "+s"(q));
+    return q;
+  };
+  auto cnt_ = [&](int i) __attribute__((always_inline)) {
+    return reinterpret_cast<uint32_t*>(scr() + kOffCnt) + (int64_t)i * kCntStride;
+  };
+  auto err_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<uint32_t*>(scr() + kOffErr); };
   uint32_t* seq = reinterpret_cast<uint32_t*>(p.scratch + kOffSeq);
   // (no err check here: it cost a memory round trip before the first load; every poll and granule sweep
   // checks err every 256 spins, so after a timeout the grid still drains within one spin round per phase)
-  uint64_t* gq = reinterpret_cast<uint64_t*>(p.scratch + kOffGq);
-  unsigned char* ob = p.scratch + kOffOb;
-  float* p1 = reinterpret_cast<float*>(p.scratch + kOffP1);
-  unsigned char* xc = p.scratch + kOffXc;
-  unsigned char* fcb = p.scratch + kOffFc;
-  float* p2 = reinterpret_cast<float*>(p.scratch + kOffP2);
+  auto gq_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<uint64_t*>(scr() + kOffGq); };
+  auto p1_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<float*>(scr() + kOffP1); };
+  auto p2_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<float*>(scr() + kOffP2); };
+  auto rsrc_of = [&](int64_t off) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(scr() + off, 0, 0x7fffffff, 0x00020000);
+  };
+  auto xc = [&]() __attribute__((always_inline)) { return scr() + kOffXc; };
   float* red = reinterpret_cast<float*>(smem + L_RED);
   float* rsum = reinterpret_cast<float*>(smem + L_STAT);
   float* rsq = rsum + 8 * 32;
@@ -278,28 +308,28 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   const int R = p.R;
   if (tid == 0) *abort_flag = 0;
   uint64_t* trace = reinterpret_cast<uint64_t*>(p.scratch + kOffTrace) + 32 * b;
-  const bool tr = ITTS_PL_TRACE && p.layer == ITTS_PL_TRACE_LAYER && tid == 0;
+  int cur_layer = p.layer;  // the model layer the loop is in (trace / debug marks)
   auto mark = [&](int i) {
-    if (tr) trace[i] = __builtin_amdgcn_s_memrealtime();
+    if (ITTS_PL_TRACE && cur_layer == ITTS_PL_TRACE_LAYER && tid == 0) trace[i] = __builtin_amdgcn_s_memrealtime();
   };
   mark(0);
   // ITTS_PL_DBG (debug builds): layer 0 of a generate's first decode step stores what wave 0 read into
   // trace slots 20..31 (profiles/lf_dbg.py)
-  const bool dbg_on = ITTS_PL_DBG && p.layer == 0 && p.tstate[0] + p.kstep == 0 && tid == 0;
+  const bool dbg_on = ITTS_PL_DBG && p.tstate[0] + p.kstep == 0 && tid == 0;
   auto dbg = [&](int i, uint32_t v) {
-    if (dbg_on) trace[20 + i] = v;
+    if (dbg_on && cur_layer == 0) trace[20 + i] = v;
   };
 
-  const int w = wave;
-  const int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
+  int w = wave;
+  int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
   const int kidx = p.kv_base + p.tstate[0] + p.kstep;
-  // this launch's epoch: a plain load (written by an earlier launch) beside the step counter's, so both are
-  // waited for together before the K/V addresses (an sc1 load at launch start was waited for on its own:
-  // +12 us per step, r05a)
-  const uint32_t L1 = *seq + 1u;
+  // this launch's first epoch: a plain load (written by an earlier launch) beside the step counter's, so both
+  // are waited for together before the K/V addresses (an sc1 load at launch start was waited for on its own:
+  // +12 us per step, r05a).  Layer i of the launch runs at epoch L1base + i.
+  const uint32_t L1base = *seq + 1u;
   // attention: this workgroup's rows of head h are 32 pt + 2 jj + u (pass pt, unit u = waves 4u .. 4u+3)
-  const int u = w >> 2;
-  const int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
+  int u = w >> 2;
+  int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
   constexpr int NG = 32;
   u32x4_t kr[KB], vr[KB];
   // K/V rows of key index jk (0-based from the row's first valid key) of row `row`: the row's own cache
@@ -307,7 +337,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   auto kv_ptr = [&](const uint16_t* cache, int row, int pos) -> const uint16_t* {
     int crow = row;
     if constexpr (ROWS) crow = p.kv_rows[(int64_t)row * p.ld_rows + pos];
-    return cache + (int64_t)crow * p.cache_bs + (int64_t)h * p.cache_hs + (int64_t)pos * kHD + 8 * d8;
+    return cache + (int64_t)crow * p.cache_bs + (int64_t)(h + zz) * p.cache_hs + (int64_t)pos * kHD + 8 * d8;
   };
   auto kv_load = [&](u32x4_t (&dst)[KB], const uint16_t* cache, int row, int p0, int nk, int j0) {
 #pragma unroll
@@ -317,12 +347,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
   };
   auto unit_row = [&](int pt) { return 32 * pt + 2 * jj + u; };
-  const int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns per tile
+  int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns per tile
+  // (phase G: wave w holds rows 4w .. 4w+3 of every row tile, xrow >> 2 == w)
 
   // ---- (A0) c_attn operands first (weights nt, 12 of 16 fragment columns real; A = x^ tile 0), then the
   // attention's first round of K/V rows (pass 0), then the residual slices, then the weight DMA
   u32x4_t bw[4], av[4][2];
-  float2 x_raw[MT];  // the residual slices, issued first (selected at phase D: no early wait on them)
+  // the residual slices (rows xrow of every tile, this thread's 2 columns): the launch's first layer loads them
+  // (issued first, selected at phase D: no early wait on them); a later layer gets them from phase G
+  float2 x_raw[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     const int row = 32 * t + xrow, xr = row < R ? row : R - 1;
@@ -334,33 +367,58 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   // waves issue the whole burst, so unit 0's later K/V rounds do not retire behind it (in-order vmcnt) -- at
   // one row per head those few units are the critical path
   const bool dma_split = ITTS_PL_DMA_SPLIT && H16 && 2 * jj < R && 2 * jj + 1 >= R;  // workgroup-uniform
-  auto dma_one = [&](int t) {
+  auto dma_one = [&](const PlLayerPtrs& Ly, int t) {
     // t is wave-uniform: each branch is one uniform DMA into its own LDS object
     if (t < 8)
-      __builtin_amdgcn_global_load_lds(p.o_w + (((int64_t)j * 64 + 8 * c + t) * 64 + lane),
+      __builtin_amdgcn_global_load_lds(Ly.o_w + (((int64_t)(j + zz) * 64 + 8 * c + t) * 64 + lane),
                                        (lds_void*)(lds_wo + t * 1024), 16, 0, WAUX);
     else if (t < 40)
-      __builtin_amdgcn_global_load_lds(p.fc_w16 + (((int64_t)(32 * c + j) * 32 + (t - 8)) * 64 + lane),
+      __builtin_amdgcn_global_load_lds(Ly.fc_w16 + (((int64_t)(32 * c + j + zz) * 32 + (t - 8)) * 64 + lane),
                                        (lds_void*)(lds_wfc + (t - 8) * 1024), 16, 0, WAUX);
     else
-      __builtin_amdgcn_global_load_lds(p.proj_w + (((int64_t)j * 256 + 32 * c + (t - 40)) * 64 + lane),
+      __builtin_amdgcn_global_load_lds(Ly.proj_w + (((int64_t)(j + zz) * 256 + 32 * c + (t - 40)) * 64 + lane),
                                        (lds_void*)(lds_wpj + (t - 40) * 1024), 16, 0, WAUX);
   };
   // straight-line issue (a data-dependent trip count leaves the compiler's vmcnt tracking a join it resolves
   // with vmcnt(0): the first key round then waited for the whole burst)
-  auto issue_dma = [&]() {
+  auto issue_dma = [&](const PlLayerPtrs& Ly) {
     if (dma_split) {
       if (w >= 4) {
 #pragma unroll
-        for (int m = 0; m < 18; ++m) dma_one(w - 4 + 4 * m);
+        for (int m = 0; m < 18; ++m) dma_one(Ly, w + zz - 4 + 4 * m);
       }
     } else {
 #pragma unroll
-      for (int m = 0; m < 9; ++m) dma_one(w + 8 * m);
+      for (int m = 0; m < 9; ++m) dma_one(Ly, w + zz + 8 * m);
     }
   };
+  // c_attn weight fragments of a layer (12 of 16 fragment columns real)
+  auto load_bw = [&](const PlLayerPtrs& Ly) {
+    const u32x4_t* wq = Ly.qkv_w12 + (int64_t)(b + zz) * 32 * 4 * kQC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = w + 8 * i;
+      if constexpr (WKEEP || ITTS_PL_KEEP_QKV)
+        bw[i] = wq[(s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0)];
+      else
+        bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
+    }
+  };
+  // the attention's first round of K/V rows (pass 0) of a layer's cache
+  auto kv_round0 = [&](const uint16_t* kc_l, const uint16_t* vc_l) {
+    const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
+    const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+    kv_load(kr, kc_l, rr, p0, nk, 0);
+    kv_load(vr, vc_l, rr, p0, nk, 0);
+  };
+  // x^ written inside this launch (phase G of the previous layer, write-through): sc1 loads
+  auto rsrc_xh = [&]() __attribute__((always_inline)) {
+    uint16_t* q = p.xh;
+    if constexpr (MULTI) asm volatile("" : "+s"(q));
+    return __builtin_amdgcn_make_buffer_rsrc(q, 0, 0x7fffffff, 0x00020000);
+  };
   {
-    const u32x4_t* wq = p.qkv_w12 + (int64_t)b * 32 * 4 * kQC;
+    const u32x4_t* wq = p.ly[0].qkv_w12 + (int64_t)b * 32 * 4 * kQC;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s = w + 8 * i;
@@ -373,25 +431,12 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!ITTS_PL_KV_LATE) {
-      const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
-      const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
-      kv_load(kr, p.kc, rr, p0, nk, 0);
-      kv_load(vr, p.vc, rr, p0, nk, 0);
-    }
+    if (!ITTS_PL_KV_LATE) kv_round0(p.kc, p.vc);
     if (ITTS_PL_DMA_EARLY) {
       __builtin_amdgcn_sched_barrier(0);
-      issue_dma();
+      issue_dma(p.ly[0]);
     }
   }
-  mark(1);
-  dbg(0, (uint32_t)kidx);
-  dbg(1, (uint32_t)(p.pad ? p.pad[0] : 0));
-  dbg(2, av[0][0][0]);
-  dbg(3, __float_as_uint(x_raw[0].x));
-  dbg(4, bw[0][0]);
-  dbg(5, kr[0][0]);
-  dbg(6, vr[0][0]);
 
   // fold statistics of one 32-row tile (the A fragments a wave accumulated): sums -> mu / rstd in LDS
   auto fold_stats = [&](const float (&ss)[2], const float (&sq)[2]) {
@@ -420,6 +465,72 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
   };
 
+  // ==== the launch's layers: layer li at epoch L1 = L1base + li.  Between two layers (the seam): every
+  // workgroup's phase G stores its x^ rows write-through and adds to CNT7; the next layer's c_attn weights and
+  // first K/V round are requested right after that add, and its x^ operands once the seam poll has matched.
+#pragma unroll 1
+  for (int li = 0; li < (MULTI ? p.nl : 1); ++li) {
+  const PlLayerPtrs& Ly = p.ly[li];
+  const uint32_t L1 = L1base + (uint32_t)li;
+  uint16_t* const kc = p.kc + (int64_t)li * p.layer_cache;
+  uint16_t* const vc = p.vc + (int64_t)li * p.layer_cache;
+  cur_layer = p.layer + li;
+  // the per-lane indices pass through an opaque copy each layer, so the compiler cannot hoist the dozens of
+  // lane addresses derived from them out of the loop (held across all layers they took every VGPR and spilled)
+  if (MULTI) {
+    asm volatile("" : "+v"(tid), "+v"(lane), "+v"(c16), "+v"(q4), "+v"(r32), "+v"(hb), "+v"(tu), "+v"(g), "+v"(d8),
+                 "+v"(xrow), "+v"(xcol));
+    // and an opaque zero that the uniform offsets (DMA sources, c_attn weights, K/V head offset) add, so they are
+    // not hoisted out of the loop either (they were, and spilled)
+    zz = 0;
+    asm volatile("" : "+s"(zz));
+    w = wave + zz;
+    u = w >> 2;
+    c = (b + zz) % kNC;
+    j = (b + zz) / kNC;
+    hh = j >> 4;
+    jj = j & 15;
+    h = 2 * c + hh;
+  }
+  if (MULTI && li > 0) {
+    mark(0);
+    if (w == 0 && lane < kNC) {  // lane q polls producer cluster q's counter for this cluster
+      const uint32_t* ctr = cnt_(CNT7 + kNC * lane + c);
+      const uint32_t target = kCPC * (L1 - 1u);
+      bool ok = true;
+      for (uint32_t n = 0;; ++n) {
+        if ((int32_t)(ld_relaxed(ctr) - target) >= 0) break;
+        if ((n & 255) == 255 && ld_relaxed(err_()) != 0) {
+          ok = false;
+          break;
+        }
+        if (n > kSpinMax) {
+          __hip_atomic_store(err_(), 7u, __ATOMIC_RELAXED, PL_SCOPE);
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!ok) *abort_flag = 1;
+    }
+    bar();
+    if (*abort_flag) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < NHF; ++t)
+        av[i][t] = __builtin_amdgcn_raw_buffer_load_b128(
+            rsrc_xh(), ((16 * t + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
+  }
+  mark(1);
+  dbg(0, (uint32_t)kidx);
+  dbg(1, (uint32_t)(p.pad ? p.pad[0] : 0));
+  dbg(2, av[0][0][0]);
+  dbg(3, __float_as_uint(x_raw[0].x));
+  dbg(4, bw[0][0]);
+  dbg(5, kr[0][0]);
+  dbg(6, vr[0][0]);
+
   // ---- (A) c_attn per 32-row tile: decode_gemm16x FOLD arithmetic (k-steps w + 8i, statistics from the
   // A fragments); q / k / v of row r, head h -> granules gq[r][h][192]; this step's k / v into the cache
 #pragma unroll 1
@@ -429,7 +540,8 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
-          av[i][hf] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4);
+          av[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
+              rsrc_xh(), ((32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
     }
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
     float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
@@ -464,13 +576,13 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
         for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
         const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = 32 * t + rt;
-        const float* uc = p.qkv_uc + (int64_t)b * 2 * kQC;
+        const float* uc = Ly.qkv_uc + (int64_t)b * 2 * kQC;
         v = fold_apply(v, rsd[rt], mu[rt], uc[col], uc[kQC + col]);
         const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
         const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
-        __hip_atomic_store(gq + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, PL_SCOPE);
+        __hip_atomic_store(gq_() + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, PL_SCOPE);
         if (i >= kHD && row < R) {  // this step's key / value into the row's own cache row (0 + v, rounded)
-          uint16_t* dst = (i < 2 * kHD ? p.kc : p.vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
+          uint16_t* dst = (i < 2 * kHD ? kc : vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
                           (int64_t)kidx * kHD + (i & (kHD - 1));
           *dst = f2bf(0.f + v);
         }
@@ -478,12 +590,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
     if (MT > 1) bar();  // red / statistics are reused by the next tile
   }
-  if (ITTS_PL_KV_LATE) {  // pass 0's K/V rows behind the c_attn operands instead of right after them
-    const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
-    const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
-    kv_load(kr, p.kc, rr, p0, nk, 0);
-    kv_load(vr, p.vc, rr, p0, nk, 0);
-  }
+  if (ITTS_PL_KV_LATE) kv_round0(kc, vc);  // pass 0's K/V rows behind the c_attn operands instead
   mark(2);
 
   // ---- (E1 + B) attention passes: unit u of pass pt = row 32 pt + 2 jj + u of head h (attn_decode_kernel
@@ -498,7 +605,6 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   constexpr int NQ = 4, GPQ = 8;
   float* qsum = pv + 32 * kPvPitch;
   float* lsum = qsum + NQ * kPvPitch;
-  auto rsrc_ob = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x7fffffff, 0x00020000);
 #pragma unroll 1
   for (int pt = 0; pt < MT; ++pt) {
     const int r_u = unit_row(pt);
@@ -506,11 +612,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     const int rr = act_u ? r_u : 0;
     const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
     if (pt > 0) {  // later passes: this pass's first round now
-      kv_load(kr, p.kc, rr, p0, nk, 0);
-      kv_load(vr, p.vc, rr, p0, nk, 0);
+      kv_load(kr, kc, rr, p0, nk, 0);
+      kv_load(vr, vc, rr, p0, nk, 0);
     }
     if ((w & 3) == 0 && act_u) {  // the unit's first wave sweeps its 192 granules
-      const uint64_t* src = gq + ((int64_t)r_u * kH + h) * 192;
+      const uint64_t* src = gq_() + ((int64_t)r_u * kH + h) * 192;
       uint64_t g0, g1, g2;
       bool ok = false;
       for (uint32_t n = 0;; ++n) {
@@ -526,12 +632,12 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           }
           break;
         }
-        if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err) != 0)) break;
+        if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err_()) != 0)) break;
         __builtin_amdgcn_s_sleep(1);
       }
       if (!ok) {
         if (lane == 0) {
-          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, PL_SCOPE);
+          __hip_atomic_store(err_(), 1u, __ATOMIC_RELAXED, PL_SCOPE);
           *abort_flag = 1;
         }
       } else {
@@ -552,7 +658,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     // granule sweep (a burst issued earlier queued in front of those loads: profiles/pl_trace_r04b.txt)
     // ITTS_PL_DMA_LATE: the burst goes out after the first key round (its K/V rows, in flight since launch
     // start, are then waited for on their own: behind an LDS-DMA the compiler can only emit vmcnt(0))
-    if (!ITTS_PL_DMA_EARLY && !ITTS_PL_DMA_LATE && pt == 0) issue_dma();
+    if (!ITTS_PL_DMA_EARLY && !ITTS_PL_DMA_LATE && pt == 0) issue_dma(Ly);
     if (act_u) {
       float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       float m_run = -INFINITY, l_run = 0.f;
@@ -597,7 +703,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           pt_ = sum8_dpp(pt_);
           sc[uu] = jk < nk ? pt_ : -INFINITY;
         }
-        if (more) kv_load(kr, p.kc, rr, p0, nk, j0 + NG * KB);
+        if (more) kv_load(kr, kc, rr, p0, nk, j0 + NG * KB);
 #pragma unroll
         for (int c0 = 0; c0 < KB; c0 += kSub) {
           float bm = -INFINITY;
@@ -625,14 +731,21 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
           }
           m_run = mn;
         }
-        if (more) kv_load(vr, p.vc, rr, p0, nk, j0 + NG * KB);
+        if (more) kv_load(vr, vc, rr, p0, nk, j0 + NG * KB);
       };
       key_round(0);  // nk >= 1: round 0 always runs
       if (ITTS_PL_DMA_LATE && !ITTS_PL_DMA_EARLY && pt == 0) {
         asm volatile("" ::: "memory");
-        issue_dma();
+        issue_dma(Ly);
       }
       if (pt == 0) mark(21);
+      // everything but the next round's 2 KB K/V rows (round 1 waits for the weight DMA whatever we do: the
+      // counter retires in order).  A compiler-visible wait: without it the DMA still pending at the loop's
+      // entry made the compiler's wait at the loop head vmcnt(0) in EVERY round (each round's V rows then
+      // waited for together with the next round's K rows; C3 step 642 -> 770 us when the layer loop came in)
+      // (small steps issue round 1 conditionally: there everything, round 1 included)
+      // (MULTI only: the single-layer form gets counted waits without it)
+      if constexpr (MULTI) __builtin_amdgcn_s_waitcnt(vm_wait_enc(ITTS_PL_KV_UNCOND && !H16 ? 2 * KB : 0));
       for (int j0 = NG * KB; j0 < nk; j0 += NG * KB) key_round(j0);
       if (pt == 0) mark(20);
 #pragma unroll
@@ -649,7 +762,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       // attention block, laid out ahead of it, and the join makes the active units' first wait vmcnt(0)
       int idle = !act_u;
       asm volatile("" : "+v"(idle)::"memory");
-      if (idle) issue_dma();
+      if (idle) issue_dma(Ly);
     }
     bar();
     if (act_u) {
@@ -685,7 +798,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     if (tu < 8) {  // o rows -> the cluster's [rows][128] tile, write-through 16-B stores
       const int d0 = 8 * tu;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
-      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_ob, ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, PL_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(kOffOb), ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, PL_AUX);
     }
     if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
@@ -694,10 +807,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   drain();  // the o stores, and this wave's weight DMA (read from LDS from phase C on)
   bar();
   mark(15);
-  if (tid == 0) add_relaxed(cnt + (CNT2 + c) * kCntStride);
+  if (tid == 0) add_relaxed(cnt_(CNT2 + c));
 
   // ---- (C) attn.c_proj split c, tile j, per 32-row tile: decode_gemm_kernel EPI 2 (one k-step per wave)
-  if (tid == 0 && !poll_ge(cnt + (CNT2 + c) * kCntStride, kCPC * L1, err, 2)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT2 + c), kCPC * L1, err_(), 2)) *abort_flag = 1;
   mark(5);
   bar();
   if (*abort_flag) return;
@@ -742,7 +855,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll 1
     for (int t = 0; t < MT; ++t) {
       const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(
-          rsrc_ob, ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, PL_AUX);
+          rsrc_of(kOffOb), ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, PL_AUX);
       f32x16_t acc32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
@@ -751,7 +864,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
       bar();
-      store_partial(p1, t);
+      store_partial(p1_(), t);
       bar();
     }
   }
@@ -759,29 +872,29 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   drain();
   bar();
   mark(16);
-  if (tid == 0) add_relaxed(cnt + (CNT3 + j) * kCntStride);
+  if (tid == 0) add_relaxed(cnt_(CNT3 + j));
 
   // ---- (D) x1 = x + (b_o + sum_c partial_c) on tile j (residual_reduce_ln_v4 order), x1^ -> cluster copy
-  if (tid == 0 && !poll_ge(cnt + (CNT3 + j) * kCntStride, kNC * L1, err, 3)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT3 + j), kNC * L1, err_(), 3)) *abort_flag = 1;
   mark(7);
   bar();
   if (*abort_flag) return;
   float2 x1[MT];
   {
-    const float2 ob2 = *reinterpret_cast<const float2*>(p.o_b + xcol);
+    const float2 ob2 = *reinterpret_cast<const float2*>(Ly.o_b + xcol);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int row = 32 * t + xrow;
       float2 pp = ob2;
 #pragma unroll
       for (int cc = 0; cc < kNC; ++cc) {
-        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p1 + ((int64_t)cc * kMaxR + row) * kD + xcol));
+        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p1_() + ((int64_t)cc * kMaxR + row) * kD + xcol));
         pp.x += __uint_as_float((uint32_t)v);
         pp.y += __uint_as_float((uint32_t)(v >> 32));
       }
       const float2 xo = row < R ? x_raw[t] : float2{0.f, 0.f};
       x1[t] = float2{xo.x + pp.x, xo.y + pp.y};
-      st_sc1_u32(reinterpret_cast<uint32_t*>(xc + (((int64_t)c * kMaxR + row) * kD + xcol) * 2),
+      st_sc1_u32(reinterpret_cast<uint32_t*>(xc() + (((int64_t)c * kMaxR + row) * kD + xcol) * 2),
                  pack2bf(x1[t].x, x1[t].y));
     }
   }
@@ -789,19 +902,20 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   drain();
   bar();
   mark(17);
-  if (tid == 0) add_relaxed(cnt + (CNT4 + c) * kCntStride);
+  if (tid == 0) add_relaxed(cnt_(CNT4 + c));
 
   // ---- (E) c_fc (ln_2 folded) + gelu on column tile 32c + j, per row tile, A = the cluster's x1^
-  if (tid == 0 && !poll_ge(cnt + (CNT4 + c) * kCntStride, kCPC * L1, err, 4)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT4 + c), kCPC * L1, err_(), 4)) *abort_flag = 1;
   // past this poll every workgroup of the grid has added at E3 (cluster c's 32 E4 adders each waited for
   // the 8 clusters of its tile), so all have read the epoch: workgroup 0 advances it for the next launch
-  if (b == 0 && tid == 0 && !*abort_flag) st_sc1_u32(seq, L1);
+  // (the next launch starts at epoch L1base + nl)
+  if (li == 0 && b == 0 && tid == 0 && !*abort_flag) st_sc1_u32(seq, L1base + (uint32_t)(p.nl - 1));
   mark(9);
   bar();
   if (*abort_flag) return;
   {
-    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(xc, 0, 0x7fffffff, 0x00020000);
-    auto rsrc_f = __builtin_amdgcn_make_buffer_rsrc(fcb, 0, 0x7fffffff, 0x00020000);
+    auto rsrc = rsrc_of(kOffXc);
+    auto rsrc_f = rsrc_of(kOffFc);
 #pragma unroll 1
     for (int t = 0; t < MT; ++t) {
       u32x4_t ax[4][2];
@@ -843,7 +957,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
         const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
         const int n = (32 * c + j) * 16 + (l & 15);
-        v = gelu_tanh_nc(fold_apply(v, rsd[rt], mu[rt], p.fc_u[n], p.fc_c[n]));
+        v = gelu_tanh_nc(fold_apply(v, rsd[rt], mu[rt], Ly.fc_u[n], Ly.fc_c[n]));
         obf[rt * 16 + (l & 15)] = f2bf(v);
       }
       bar();
@@ -860,15 +974,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   drain();
   bar();
   mark(18);
-  if (tid == 0) add_relaxed(cnt + (CNT5 + c) * kCntStride);
+  if (tid == 0) add_relaxed(cnt_(CNT5 + c));
 
   // ---- (F) mlp.c_proj split c, tile j, per row tile: decode_gemm_kernel EPI 2 (k-steps w + 8i of the split)
-  if (tid == 0 && !poll_ge(cnt + (CNT5 + c) * kCntStride, kCPC * L1, err, 5)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT5 + c), kCPC * L1, err_(), 5)) *abort_flag = 1;
   mark(11);
   bar();
   if (*abort_flag) return;
   {
-    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(fcb, 0, 0x7fffffff, 0x00020000);
+    auto rsrc = rsrc_of(kOffFc);
 #pragma unroll 1
     for (int t = 0; t < MT; ++t) {
       u32x4_t a4[4];
@@ -887,7 +1001,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
       bar();
-      store_partial(p2, t);
+      store_partial(p2_(), t);
       bar();
     }
   }
@@ -895,25 +1009,30 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   drain();
   bar();
   mark(19);
-  if (tid == 0) add_relaxed(cnt + (CNT6 + j) * kCntStride);
+  if (tid == 0) add_relaxed(cnt_(CNT6 + j));
 
-  // ---- (G) x2 = x1 + (b_proj + sum_c partial_c); x, x^ for the next launch (cluster c: rows 4c .. 4c+3 of
-  // every tile).  The last layer stores x1 and leaves this reduce (with ln_f + final_norm, Q5) to
-  // itts_residual_reduce_ln over the partials.
-  if (p.last) {
+  // ---- (G) x2 = x1 + (b_proj + sum_c partial_c) on tile j.  Wave c (rows 4c .. 4c+3 of every tile) stores x^
+  // for the next layer (write-through: the seam) and, at the launch's end, x; inside the launch every wave keeps
+  // its rows' x2 as the next layer's residual slices.  The model's last layer stores x1 and leaves this reduce
+  // (with ln_f + final_norm, Q5) to itts_residual_reduce_ln over the partials.  Every layer adds to the seam
+  // counters (each CNT7 counter holds 32 x the epoch after it).
+  const bool more_layers = MULTI && li + 1 < p.nl;
+  if (p.last && !more_layers) {
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int row = 32 * t + xrow;
       if ((xrow >> 2) == c && row < R) *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x1[t];
     }
+    if (p.seam && w == 0 && lane < kNC) add_relaxed(cnt_(CNT7 + kNC * c + lane));
     return;
   }
-  if (tid == 0 && !poll_ge(cnt + (CNT6 + j) * kCntStride, kNC * L1, err, 6)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT6 + j), kNC * L1, err_(), 6)) *abort_flag = 1;
   mark(13);
   bar();
   if (*abort_flag) return;
-  if ((xrow >> 2) == c) {
-    const float2 pb2 = *reinterpret_cast<const float2*>(p.proj_b + xcol);
+  // x2 of this wave's rows (4w .. 4w+3 of every row tile) -> x_raw; wave c stores them
+  auto g_rows = [&](bool store) __attribute__((always_inline)) {
+    const float2 pb2 = *reinterpret_cast<const float2*>(Ly.proj_b + xcol);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int row = 32 * t + xrow;
@@ -921,16 +1040,40 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       float2 pp = pb2;
 #pragma unroll
       for (int cc = 0; cc < kNC; ++cc) {
-        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p2 + ((int64_t)cc * kMaxR + row) * kD + xcol));
+        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p2_() + ((int64_t)cc * kMaxR + row) * kD + xcol));
         pp.x += __uint_as_float((uint32_t)v);
         pp.y += __uint_as_float((uint32_t)(v >> 32));
       }
       const float2 x2 = float2{x1[t].x + pp.x, x1[t].y + pp.y};
-      *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x2;
-      *reinterpret_cast<uint32_t*>(p.xh + (int64_t)row * kD + xcol) = pack2bf(x2.x, x2.y);
+      x_raw[t] = x2;
+      if (store) {
+        if (!more_layers) *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x2;
+        const uint32_t pk = pack2bf(x2.x, x2.y);
+        if (MULTI) {  // 8 columns (4 lanes) per 16-B write-through store: a narrow sc1 store is one fabric write
+          const uint32_t n1 = __shfl_down(pk, 1, 64), n2 = __shfl_down(pk, 2, 64), n3 = __shfl_down(pk, 3, 64);
+          if ((lane & 3) == 0)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{pk, n1, n2, n3}, rsrc_xh(), (row * kD + xcol) * 2, 0, PL_AUX);
+        } else {
+          *reinterpret_cast<uint32_t*>(p.xh + (int64_t)row * kD + xcol) = pk;
+        }
+      }
     }
+  };
+  if (w == c) g_rows(true);
+  if (MULTI) {
+    if (w == c) drain();  // the x^ stores (write-through) have left before the seam add
+    bar();
   }
+  if ((MULTI || p.seam) && w == 0 && lane < kNC) add_relaxed(cnt_(CNT7 + kNC * c + lane));
   mark(14);
+  if (more_layers) {
+    // the other waves' residual rows for the next layer (off the seam's critical path: after the add), then the
+    // next layer's c_attn weights and first K/V round, in flight across the seam
+    if (w != c) g_rows(false);
+    load_bw(p.ly[li + 1]);
+    if (!ITTS_PL_KV_LATE) kv_round0(kc + p.layer_cache, vc + p.layer_cache);
+  }
+  }  // layers
 }
 
 int g_cu_count = -1;
@@ -963,7 +1106,9 @@ extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, true>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, false>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, true>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>)};
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>),
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKB, false, false, true>),
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, true>)};
     for (const void* k : ks) {
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess || nb < 1) occ = 0;
@@ -990,35 +1135,55 @@ extern "C" int itts_gpt_pl_error(const void* scratch, void* stream, int* code) {
   return 0;
 }
 
-extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl, const ItTsGptDecodeState* st,
-                                 int layer, int kstep, int last, void* scratch, void* stream) {
-  const char* fn = "itts_gpt_layer_pl";
-  ITTS_REQUIRE(ly && pl && st && scratch, fn, "null pointer");
-  ITTS_REQUIRE(pl->qkv_w12 && pl->qkv_uc && ly->o_w && ly->fc_w16 && ly->fc_u && ly->fc_c && ly->proj_w &&
-                   ly->proj_b && ly->o_c,
-               fn, "incomplete layer weights");
-  ITTS_REQUIRE(st->rows >= 1 && st->rows <= kMaxR, fn, "1..128 rows");
-  ITTS_REQUIRE(!st->kv_rows || st->ld_rows >= st->max_kv, fn, "kv_rows [rows][ld_rows >= max_kv]");
-  ITTS_REQUIRE(st->x && st->xh && st->k_cache && st->v_cache && st->tstate, fn, "null state buffer");
-  ITTS_REQUIRE((reinterpret_cast<uintptr_t>(scratch) & 255) == 0, fn, "scratch must be 256-B aligned");
+namespace {
+// layers per persistent launch (ITTS_PL_LPL; default 1 = one launch per layer).  The multi-layer form (layers
+// joined inside the launch by the CNT7 seam, the next layer's c_attn weights and first K/V round requested across
+// it) is bit-identical and measured SLOWER: C3 decode step 714 vs 647 us, C2 547 vs 513 us (profiles/
+// pl_trace_r05o_lpl*.txt): the seam (x2 reduce by one wave, 16-B write-through x^ stores, drain, 8 x 8 replicated
+// counters, poll, 64 KiB of x^ per workgroup read back from the memory side) costs more than the kernel boundary
+// it replaces (G -> next layer's operands issued: 5.8 vs 3.8 us)
+int layers_per_launch() {
+  static const int n = [] {
+    const char* e = getenv("ITTS_PL_LPL");
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : (v > kMaxLpl ? kMaxLpl : v);
+  }();
+  return n;
+}
+
+PlLayerPtrs layer_ptrs(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl) {
+  PlLayerPtrs q;
+  q.qkv_w12 = static_cast<const u32x4_t*>(pl->qkv_w12);
+  q.qkv_uc = pl->qkv_uc;
+  q.o_w = static_cast<const u32x4_t*>(ly->o_w);
+  q.o_b = ly->o_c;
+  q.fc_w16 = static_cast<const u32x4_t*>(ly->fc_w16);
+  q.fc_u = ly->fc_u;
+  q.fc_c = ly->fc_c;
+  q.proj_w = static_cast<const u32x4_t*>(ly->proj_w);
+  q.proj_b = ly->proj_b;
+  return q;
+}
+
+bool layer_ok(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl) {
+  return ly && pl && pl->qkv_w12 && pl->qkv_uc && ly->o_w && ly->fc_w16 && ly->fc_u && ly->fc_c && ly->proj_w &&
+         ly->proj_b && ly->o_c;
+}
+
+// layers layer .. layer + nl - 1 (weights ly[0 .. nl-1]) of decode step kstep as ONE launch
+int launch_layers(const ItTsGptLayerW* const* lyw, const ItTsGptPlLayerW* const* plw, const ItTsGptDecodeState* st,
+                  int layer, int nl, int kstep, int last, bool keep, void* scratch, hipStream_t s, const char* fn) {
   const int64_t cache_hs = (int64_t)st->max_kv * kHD, cache_bs = (int64_t)kH * cache_hs;
   const int64_t layer_cache = (int64_t)st->rows * cache_bs;
-  PlArgs a;
-  a.qkv_w12 = static_cast<const u32x4_t*>(pl->qkv_w12);
-  a.qkv_uc = pl->qkv_uc;
-  a.o_w = static_cast<const u32x4_t*>(ly->o_w);
-  a.o_b = ly->o_c;
-  a.fc_w16 = static_cast<const u32x4_t*>(ly->fc_w16);
-  a.fc_u = ly->fc_u;
-  a.fc_c = ly->fc_c;
-  a.proj_w = static_cast<const u32x4_t*>(ly->proj_w);
-  a.proj_b = ly->proj_b;
+  PlArgsT<kMaxLpl> a;
+  for (int i = 0; i < nl; ++i) a.ly[i] = layer_ptrs(lyw[i], plw[i]);
   a.x = st->x;
   a.xh = static_cast<uint16_t*>(st->xh);
   a.kc = static_cast<uint16_t*>(st->k_cache) + layer * layer_cache;
   a.vc = static_cast<uint16_t*>(st->v_cache) + layer * layer_cache;
   a.cache_bs = cache_bs;
   a.cache_hs = cache_hs;
+  a.layer_cache = layer_cache;
   a.pad = st->pad;
   a.tstate = st->tstate;
   a.kv_rows = st->kv_rows;
@@ -1027,46 +1192,65 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   a.kstep = kstep;
   a.R = st->rows;
   a.layer = layer;
+  a.nl = nl;
   a.last = last;
+  a.seam = layers_per_launch() > 1;  // CNT7 counts stay n x epoch only if every launch of the process adds
   a.eps = 1e-5f;
   a.scratch = static_cast<unsigned char*>(scratch);
+  PlArgsT<1> a1;
+  static_cast<PlCommon&>(a1) = a;
+  a1.ly[0] = a.ly[0];
   const int mt = (st->rows + 31) / 32;
-  const void* fnp = nullptr;
-#define PL_K(MTV, RW) reinterpret_cast<const void*>(gpt_layer_pl_kernel<MTV, RW>)
-  switch (mt) {
-    case 1: fnp = st->kv_rows ? PL_K(1, true) : PL_K(1, false); break;
-    case 2: fnp = st->kv_rows ? PL_K(2, true) : PL_K(2, false); break;
-    case 3: fnp = st->kv_rows ? PL_K(3, true) : PL_K(3, false); break;
-    default: fnp = st->kv_rows ? PL_K(4, true) : PL_K(4, false); break;
-  }
-#undef PL_K
-  (void)fnp;
   const int ki = 2 * (mt - 1) + (st->kv_rows ? 1 : 0);
-  hipStream_t s = itts::as_stream(stream);
-  const bool keep = layer < keep_layers();
   if (ki == 0 && st->rows <= kSmallRows) {  // kSmallRows <= 16: one 16-row half
-    if (keep)
-      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, true, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s, a);
+    if (nl > 1)
+      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, true>), dim3(kWG), dim3(kThreads), 0,
+                         s, a);
+    else if (keep)
+      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, true, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s, a1);
     else
       hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s,
-                         a);
+                         a1);
     return itts::check_launch(fn);
   }
   if (ki == 0 && keep) {
-    hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKB, true>), dim3(kWG), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKB, true>), dim3(kWG), dim3(kThreads), 0, s, a1);
+    return itts::check_launch(fn);
+  }
+  if (ki == 0 && nl > 1) {
+    hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKB, false, false, true>), dim3(kWG), dim3(kThreads), 0, s, a);
     return itts::check_launch(fn);
   }
   switch (ki) {
-    case 0: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
-    case 5: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
-    case 6: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
-    default: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    case 1: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    case 2: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    case 3: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    case 4: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    case 5: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    case 6: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    default: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
   }
   return itts::check_launch(fn);
+}
+
+int check_state(const ItTsGptDecodeState* st, void* scratch, const char* fn) {
+  ITTS_REQUIRE(st->rows >= 1 && st->rows <= kMaxR, fn, "1..128 rows");
+  ITTS_REQUIRE(!st->kv_rows || st->ld_rows >= st->max_kv, fn, "kv_rows [rows][ld_rows >= max_kv]");
+  ITTS_REQUIRE(st->x && st->xh && st->k_cache && st->v_cache && st->tstate, fn, "null state buffer");
+  ITTS_REQUIRE((reinterpret_cast<uintptr_t>(scratch) & 255) == 0, fn, "scratch must be 256-B aligned");
+  return 0;
+}
+}  // namespace
+
+extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl, const ItTsGptDecodeState* st,
+                                 int layer, int kstep, int last, void* scratch, void* stream) {
+  const char* fn = "itts_gpt_layer_pl";
+  ITTS_REQUIRE(ly && pl && st && scratch, fn, "null pointer");
+  ITTS_REQUIRE(layer_ok(ly, pl), fn, "incomplete layer weights");
+  if (int rc = check_state(st, scratch, fn)) return rc;
+  return launch_layers(&ly, &pl, st, layer, 1, kstep, last, layer < keep_layers(), scratch, itts::as_stream(stream),
+                       fn);
 }
 
 // Re-arm the scratch: counters, every granule, the epoch and the error word to zero.  An ordinary kernel
@@ -1106,10 +1290,27 @@ extern "C" int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPl
   ITTS_REQUIRE(st->logits && w->head_w && (smp->mode == 2 || (st->seen && st->done && st->codes)), fn,
                "sampler state missing");
   const int L = w->n_layer, D = w->d_model, R = st->rows;
+  if (int rc = check_state(st, scratch, fn)) return rc;
+  for (int l = 0; l < L; ++l) ITTS_REQUIRE(layer_ok(&w->layers[l], &pl[l]), fn, "incomplete layer weights");
+  // the step's layers in launches of up to layers_per_launch() (the keep-policy layers in launches of their own)
+  const ItTsGptLayerW* lyw[kMaxLpl];
+  const ItTsGptPlLayerW* plw[kMaxLpl];
+  const int nkeep = keep_layers();
+  const int lpl = (R <= 32 && !st->kv_rows) ? layers_per_launch() : 1;
+  hipStream_t s = itts::as_stream(stream);
   int rc = 0;
   for (int k = 0; k < nsteps && rc == 0; ++k) {
-    for (int l = 0; l < L && rc == 0; ++l)
-      rc = itts_gpt_layer_pl(&w->layers[l], &pl[l], st, l, k, l + 1 == L, scratch, stream);
+    for (int l0 = 0; l0 < L && rc == 0;) {
+      const bool keep = l0 < nkeep;
+      int nl = L - l0 < lpl ? L - l0 : lpl;
+      if (keep && l0 + nl > nkeep) nl = nkeep - l0;
+      for (int i = 0; i < nl; ++i) {
+        lyw[i] = &w->layers[l0 + i];
+        plw[i] = &pl[l0 + i];
+      }
+      rc = launch_layers(lyw, plw, st, l0, nl, k, l0 + nl == L, keep, scratch, s, fn);
+      l0 += nl;
+    }
     // the last layer's mlp.c_proj reduce with ln_f + final_norm (Q5) over the persistent partials
     if (rc == 0)
       rc = itts_residual_reduce_ln(st->x, D, reinterpret_cast<float*>(static_cast<unsigned char*>(scratch) + kOffP2),

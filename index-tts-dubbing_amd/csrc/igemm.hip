@@ -284,22 +284,24 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 template <int TN, int WAVES_M, int WAVES_N, int BK, int NSLOT, typename OutT, bool WIN = false>
-__global__ __launch_bounds__(512) void igemm256_kernel(IgArgs p) {
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void igemm256_kernel(IgArgs p) {
+  constexpr int NW = WAVES_M * WAVES_N;  // 8 waves of 128 x 64 (or 64 x 96 ...), or 4 of 128 x 128
   constexpr int TM = 256, ROWB = BK * 2, SPR = BK / 8, RPI = 1024 / ROWB;  // 16-B slots per row, rows per DMA
   constexpr int D = NSLOT - 1;  // K steps in flight ahead of the one computed
   constexpr int WM = TM / WAVES_M, WN = TN / WAVES_N, FM = WM / 32, FN = WN / 32;
   constexpr int A_BYTES = TM * ROWB, B_BYTES = TN * ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INS = TM / RPI / 8, B_INS = TN / RPI / 8;  // DMA instructions per wave per K step
+  constexpr int A_INS = TM / RPI / NW, B_INS = TN / RPI / NW;  // DMA instructions per wave per K step
   constexpr int P = A_INS + B_INS;
   constexpr int EP = WN + 4;  // epilogue staging pitch (floats): rows r and r + 4 on other banks
   // WIN (convs of >= 3 taps): K steps run channel chunk outer, tap inner; a chunk's A operand is ONE
   // window of TM + kWinSpan input rows, in its own double buffer, and a K step moves only B.  The next
   // chunk's window is issued at the first step of a chunk, after that step's B, so it may stay in flight
   // across one barrier (counted vmcnt) and lands during the chunk's taps.
-  constexpr int WROWS = TM + kWinSpan, W_BYTES = WROWS * ROWB, W_INS = WROWS / RPI / 8;
-  static_assert(WAVES_M * WAVES_N == 8 && B_INS >= 1 && (BK == 32 || BK == 64) && D >= 1, "geometry");
-  static_assert(!WIN || (NSLOT == 2 && WROWS % (RPI * 8) == 0), "window form: double-buffered B");
-  static_assert(8 * 32 * EP * 4 <= (WIN ? 2 * (W_BYTES + B_BYTES) : NSLOT * STAGE), "epilogue staging fits");
+  constexpr int WROWS = TM + kWinSpan, W_BYTES = WROWS * ROWB, W_INS = WROWS / RPI / NW;
+  static_assert((NW == 8 || NW == 4) && B_INS >= 1 && (BK == 32 || BK == 64) && D >= 1, "geometry");
+  static_assert(A_INS * RPI * NW == TM && B_INS * RPI * NW == TN, "whole DMA instructions per wave");
+  static_assert(!WIN || (NSLOT == 2 && WROWS % (RPI * NW) == 0), "window form: double-buffered B");
+  static_assert(NW * 32 * EP * 4 <= (WIN ? 2 * (W_BYTES + B_BYTES) : NSLOT * STAGE), "epilogue staging fits");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // slot permutation of a row (an involution on the row's SPR slots): 16 consecutive rows of a fragment
   // read fall on 16 distinct bank quads
@@ -599,12 +601,14 @@ void launch256(const IgArgs& a, hipStream_t s) {
   if constexpr (NSLOT == 2 && BK == 64) {
     if (a.ntaps >= ITTS_IG_WIN_MINTAPS && a.span <= kWinSpan && igemm_win_enabled()) {
       const size_t lds = 2 * (size_t)(256 + kWinSpan + TN) * 2 * BK;
-      hipLaunchKernelGGL((igemm256_kernel<TN, WAVES_M, WAVES_N, BK, 2, OutT, true>), grid, dim3(512), lds, s, a);
+      hipLaunchKernelGGL((igemm256_kernel<TN, WAVES_M, WAVES_N, BK, 2, OutT, true>), grid, dim3(64 * WAVES_M * WAVES_N),
+                         lds, s, a);
       return;
     }
   }
   const size_t lds = (size_t)NSLOT * (256 + TN) * 2 * BK;
-  hipLaunchKernelGGL((igemm256_kernel<TN, WAVES_M, WAVES_N, BK, NSLOT, OutT>), grid, dim3(512), lds, s, a);
+  hipLaunchKernelGGL((igemm256_kernel<TN, WAVES_M, WAVES_N, BK, NSLOT, OutT>), grid, dim3(64 * WAVES_M * WAVES_N), lds,
+                     s, a);
 }
 // tile variant (ITTS_IG256_VARIANT, A/B; profiles/ubench_igemm256_r03.txt): 0 = K steps of 32 (64-B rows),
 // 4-slot ring, 3 steps in flight; 1 = 256 x 128, K steps of 64, 3 slots; 2 = 256 x 256 K steps of 64
@@ -690,6 +694,12 @@ void dispatch(const IgArgs& a, bool vec, hipStream_t s) {
       if (k64 && a.Cout == 192 && ig192_enabled()) launch256<192, 4, 2, 64, 2, OutT>(a, s);
       else if (k64) launch256<64, 4, 2, 64, 2, OutT>(a, s);
       else dispatch_old<OutT>(a, vec, s);
+      return;
+    }
+    // 4 (A/B): 4 waves of 128 x 128 (half the LDS fragment reads per flop, one wave per SIMD, 256 VGPRs + 256
+    // AGPRs): measured 30-40 % SLOWER on every latent GEMM (c_attn 227 vs 158 us, c_fc 364 vs 237, profiles/r05_ig.sh)
+    if (v == 4 && k64 && a.Cout % 256 == 0) {
+      launch256<256, 2, 2, 64, 2, OutT>(a, s);
       return;
     }
     if (v == 1 && k64) launch256<128, 4, 2, 64, 3, OutT>(a, s);
