@@ -342,7 +342,8 @@ def main():
         d_bytes = sum(tts.gpt.step_weight_bytes + keys * tts.gpt.kv_bytes_per_key for _, _, _, keys in step_ev)
         gbs = d_bytes / (d_ms * 1e-3) / 1e9
         rows = step_ev[0][2]
-        pl = bool(tts.gpt.pl and tts.gpt._pl_ok({"B": rows}))
+        pl_st = {"B": rows, "kv_rows": True} if args.decoding == "beam3" else {"B": rows}
+        pl = bool(tts.gpt.pl and tts.gpt._pl_ok(pl_st))
         body = ("20 x ONE persistent launch per layer (gpt_layer.hip: c_attn (ln_1 folded) -> attention -> "
                 "attn.c_proj split-K 8 + reduce -> c_fc (ln_2 folded, gelu) -> mlp.c_proj split-K 8 + reduce as "
                 "phases joined by in-launch hand-offs (epoch-tagged, nothing reset per step), weights prefetched "

@@ -80,6 +80,7 @@ constexpr int kSub = 4;  // keys per group per online-softmax update (every KB i
 #ifndef ITTS_KV_NT
 #define ITTS_KV_NT 1
 #endif
+constexpr int kAttnKviMax = 3584;  // beams: keys per row whose lineage indices the kernel stages in LDS
 template <typename TC, typename TO, int NT, bool ROWS, bool PROJ, int KB = ITTS_ATTN_KB>
 __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
                                                          int64_t split_stride, const float* __restrict__ qkv_bias,
@@ -106,9 +107,16 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
   TC* Kc = cache_k + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
   TC* Vc = cache_v + (int64_t)b * cache_bs + (int64_t)h * cache_hs;
   const int32_t* rows = ROWS ? kv_rows + (int64_t)b * ld_rows : nullptr;
+  // ROWS: the row's lineage indices of keys p0 .. kidx staged in LDS first, so a round's K/V addresses need an
+  // LDS read instead of a global load (whose in-order vmcnt wait also waited for the previous round's V rows)
+  __shared__ int32_t rws[ROWS ? kAttnKviMax : 1];
+  if constexpr (ROWS) {
+    for (int i = threadIdx.x; i < nk; i += NT) rws[i] = rows[p0 + i];
+    __syncthreads();
+  }
   // element offset of key position p (relative to Kc / Vc)
   auto koff = [&](int p) -> int64_t {
-    if constexpr (ROWS) return (int64_t)(rows[p] - b) * cache_bs + (int64_t)p * kHD;
+    if constexpr (ROWS) return (int64_t)(rws[p - p0] - b) * cache_bs + (int64_t)p * kHD;
     else return (int64_t)p * kHD;
   };
   const int g = threadIdx.x >> 3, d8 = threadIdx.x & 7;
@@ -582,6 +590,7 @@ int attn_decode_launch(const char* fn, const float* qkv, int64_t ldqkv, int nspl
   if (B == 0) return 0;
   ITTS_REQUIRE(qkv && cache_k && cache_v && tstate && (out || wproj), fn, "null pointer");
   ITTS_REQUIRE(smax <= kMaxKeys && cache_hs >= (int64_t)smax * kHD, fn, "bad cache capacity");
+  ITTS_REQUIRE(!kv_rows || smax <= kAttnKviMax, fn, "beam decoding: at most 3584 keys per row (LDS lineage)");
   ITTS_REQUIRE(!wproj || (part && N > 0 && N <= 1024 && N % 8 == 0 && ldp >= N && ldp % 4 == 0 &&
                           part_stride % 4 == 0 &&
                           ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(wproj)) & 15) == 0),
@@ -655,6 +664,7 @@ extern "C" int itts_attn_decode_proj(const float* qkv, int64_t ldqkv, int nsplit
   const char* fn = "itts_attn_decode_proj";
   ITTS_REQUIRE(w_proj, fn, "w_proj required");
   ITTS_REQUIRE(!kv_rows || ld_rows >= smax, fn, "kv_rows [B][ld_rows >= smax] required");
+  ITTS_REQUIRE(!kv_rows || smax <= kAttnKviMax, fn, "beam decoding: at most 3584 keys per row");
   return attn_decode_launch(fn, qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v, cache_bs, cache_hs,
                             smax, pad, kv_base, tstate, nullptr, 0, B, H, cache_dtype, ITTS_F32, kv_rows, ld_rows,
                             w_proj, N, part, part_stride, ldp, stream);
@@ -667,6 +677,7 @@ extern "C" int itts_attn_decode_rows(const float* qkv, int64_t ldqkv, int nsplit
                                      int out_dtype, const int32_t* kv_rows, int64_t ld_rows, void* stream) {
   const char* fn = "itts_attn_decode_rows";
   ITTS_REQUIRE(kv_rows && ld_rows >= smax, fn, "kv_rows [B][ld_rows >= smax] required");
+  ITTS_REQUIRE(smax <= kAttnKviMax, fn, "beam decoding: at most 3584 keys per row");
   return attn_decode_launch(fn, qkv, ldqkv, nsplit, split_stride, qkv_bias, cache_k, cache_v, cache_bs, cache_hs,
                             smax, pad, kv_base, tstate, out, ldo, B, H, cache_dtype, out_dtype, kv_rows, ld_rows,
                             nullptr, 0, nullptr, 0, 0, stream);

@@ -188,6 +188,10 @@ struct PlLayerPtrs {
   const float* proj_b;
 };
 constexpr int kMaxLpl = 32;  // layers per launch (kernel-argument table; 32 x 72 B)
+// beams (kv_rows): each attention unit stages its row's lineage indices (keys 0 .. nk-1) in LDS, so a key
+// round's K/V addresses need an LDS read, not a global load whose vmcnt wait (in order) also waited for the
+// round's V rows still in flight; max_kv of a beam state must not exceed this
+constexpr int kKviMax = 3584;
 struct PlCommon {
   float* x;                // [R][1024] f32
   uint16_t* xh;            // [32][1024] bf16 (rows >= R: read, never written)
@@ -215,6 +219,7 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
+constexpr int kDropLimit = 0x7fff0000, kDrop = 0x7ffffff0;  // cancelled buffer stores (see rsrc_of_lim)
 // s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= n only (expcnt / lgkmcnt at their maxima)
 constexpr int vm_wait_enc(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 // every storing wave's write-through stores have left (Guideline 16 R1: before the counter add)
@@ -268,6 +273,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   __shared__ __attribute__((aligned(16))) unsigned char lds_wfc[32 * 1024];
   __shared__ __attribute__((aligned(16))) unsigned char lds_wpj[32 * 1024];
   __shared__ __attribute__((aligned(16))) unsigned char lds_rest[kRestBytes];
+  __shared__ int32_t lds_kvi[ROWS ? 2 * kKviMax : 1];  // [unit][key] lineage cache rows (beams)
   unsigned char* const smem = lds_rest - L_RED;  // offsets >= L_RED address lds_rest
   typedef __attribute__((address_space(3))) void lds_void;
   const int b = blockIdx.x;
@@ -298,6 +304,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
     return __builtin_amdgcn_make_buffer_rsrc(scr() + off, 0, 0x7fffffff, 0x00020000);
   };
   auto xc = [&]() __attribute__((always_inline)) { return scr() + kOffXc; };
+  // descriptors whose stores a lane can cancel: range kDropLimit, and a cancelled lane's offset kDrop lies past it
+  // (offset >= range and offset + size > range: dropped under either bounds rule)
+  auto rsrc_of_lim = [&](int64_t off) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(scr() + off, 0, kDropLimit, 0x00020000);
+  };
   float* red = reinterpret_cast<float*>(smem + L_RED);
   float* rsum = reinterpret_cast<float*>(smem + L_STAT);
   float* rsq = rsum + 8 * 32;
@@ -334,19 +345,28 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   u32x4_t kr[KB], vr[KB];
   // K/V rows of key index jk (0-based from the row's first valid key) of row `row`: the row's own cache
   // row, or (beams) the row of kv_rows[row][position] that holds that prefix position
-  auto kv_ptr = [&](const uint16_t* cache, int row, int pos) -> const uint16_t* {
+  auto kv_ptr = [&](const uint16_t* cache, int row, int pos, int jk) -> const uint16_t* {
     int crow = row;
-    if constexpr (ROWS) crow = p.kv_rows[(int64_t)row * p.ld_rows + pos];
+    if constexpr (ROWS) crow = lds_kvi[u * kKviMax + jk];
     return cache + (int64_t)crow * p.cache_bs + (int64_t)(h + zz) * p.cache_hs + (int64_t)pos * kHD + 8 * d8;
   };
   auto kv_load = [&](u32x4_t (&dst)[KB], const uint16_t* cache, int row, int p0, int nk, int j0) {
 #pragma unroll
     for (int uu = 0; uu < KB; ++uu) {
       const int jk = min(j0 + NG * uu + g, max(nk - 2, 0));
-      dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk)));
+      dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk, jk)));
     }
   };
   auto unit_row = [&](int pt) { return 32 * pt + 2 * jj + u; };
+  // beams: this unit's lineage indices of row `row` (keys 0 .. nk-1) into LDS; every thread of the workgroup
+  // calls it (it ends with the barrier the readers need)
+  auto stage_kvi = [&](int row, int p0, int nk) __attribute__((always_inline)) {
+    if constexpr (ROWS) {
+      const int32_t* src = p.kv_rows + (int64_t)row * p.ld_rows + p0;
+      for (int i = tu; i < nk; i += 256) lds_kvi[u * kKviMax + i] = src[i];
+      bar();
+    }
+  };
   int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns per tile
   // (phase G: wave w holds rows 4w .. 4w+3 of every row tile, xrow >> 2 == w)
 
@@ -408,6 +428,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   auto kv_round0 = [&](const uint16_t* kc_l, const uint16_t* vc_l) {
     const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
     const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+    stage_kvi(rr, p0, nk);
     kv_load(kr, kc_l, rr, p0, nk, 0);
     kv_load(vr, vc_l, rr, p0, nk, 0);
   };
@@ -533,15 +554,27 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
 
   // ---- (A) c_attn per 32-row tile: decode_gemm16x FOLD arithmetic (k-steps w + 8i, statistics from the
   // A fragments); q / k / v of row r, head h -> granules gq[r][h][192]; this step's k / v into the cache
-#pragma unroll 1
+  // row tiles > 0 (beams, long-form chunks): the next tile's A fragments are requested before this tile's
+  // MFMAs (double-buffered; loaded inside the loop they were one serial round trip per tile: c_attn 8.8 us
+  // at 3 tiles, profiles/pl_trace_r05q_96.txt)
+  u32x4_t avn[4][2];
+  // the lane's fold terms (every row tile's), loaded ahead of the prefetches: an epilogue load behind them made
+  // the tile's stores wait for the next tile's A fragments (in-order vmcnt)
+  float uc0 = 0.f, uc1 = 0.f;
+  if constexpr (MT > 1) {
+    const int cq = (lane & 15) < kQC ? (lane & 15) : 0;
+    uc0 = Ly.qkv_uc[(int64_t)b * 2 * kQC + cq];
+    uc1 = Ly.qkv_uc[(int64_t)b * 2 * kQC + kQC + cq];
+  }
+#pragma unroll  // (MT > 1: straight-line tiles, so the compiler's vmcnt counts stay exact across them)
   for (int t = 0; t < MT; ++t) {
-    if (t > 0) {
+    if (MT > 1 && t + 1 < MT) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
-          av[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
-              rsrc_xh(), ((32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
+          avn[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
+              rsrc_xh(), ((32 * (t + 1) + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
     }
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
     float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
@@ -569,7 +602,33 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
     bar();
     mu_rs();
     bar();
-    {  // one output per thread: 32 rows x 16 fragment columns (12 real)
+    if constexpr (MT > 1) {
+      // several row tiles: the same outputs, but every store instruction issued by every wave (lanes with no
+      // output get an offset past the buffer's range: the hardware drops them), so the compiler counts the
+      // stores exactly and waits for the next tile's A fragments without waiting for these write-through stores
+      // (with lane-conditional stores its wait at the tile loop's head was vmcnt(0))
+      const int e = tid >> 6, l = lane, col = l & 15;
+      const bool ok = col < kQC;
+      const int cq = ok ? col : 0;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
+      const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = 32 * t + rt;
+      v = fold_apply(v, rsd[rt], mu[rt], uc0, uc1);
+      const int i = kQC * jj + cq;
+      const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
+      const int goff = ok ? (((row * kH + h) * 192 + i) * 8) : kDrop;
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{(uint32_t)gr, (uint32_t)(gr >> 32)},
+                                            __builtin_amdgcn_make_buffer_rsrc(gq_(), 0, kDropLimit, 0x00020000), goff,
+                                            0, PL_AUX);
+      const int coff = (row * (int)p.cache_bs + h * (int)p.cache_hs + kidx * kHD + (i & (kHD - 1))) * 2;
+      const bool kv_ok = ok && row < R;
+      const uint16_t hv = f2bf(0.f + v);
+      __builtin_amdgcn_raw_buffer_store_b16(hv, __builtin_amdgcn_make_buffer_rsrc(kc, 0, kDropLimit, 0x00020000),
+                                            kv_ok && i >= kHD && i < 2 * kHD ? coff : kDrop, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(hv, __builtin_amdgcn_make_buffer_rsrc(vc, 0, kDropLimit, 0x00020000),
+                                            kv_ok && i >= 2 * kHD ? coff : kDrop, 0, 0);
+    } else {  // one output per thread: 32 rows x 16 fragment columns (12 real)
       const int e = tid >> 6, l = lane, col = l & 15;
       if (col < kQC) {
         float v = 0.f;
@@ -588,7 +647,13 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
         }
       }
     }
-    if (MT > 1) bar();  // red / statistics are reused by the next tile
+    if (MT > 1) {
+      bar();  // red / statistics are reused by the next tile
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) av[i][hf] = avn[i][hf];
+    }
   }
   if (ITTS_PL_KV_LATE) kv_round0(kc, vc);  // pass 0's K/V rows behind the c_attn operands instead
   mark(2);
@@ -612,6 +677,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
     const int rr = act_u ? r_u : 0;
     const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
     if (pt > 0) {  // later passes: this pass's first round now
+      stage_kvi(rr, p0, nk);
       kv_load(kr, kc, rr, p0, nk, 0);
       kv_load(vr, vc, rr, p0, nk, 0);
     }
@@ -852,10 +918,14 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   };
   {
     const u32x4_t bb = *reinterpret_cast<const u32x4_t*>(lds_wo + w * 1024 + lane * 16);
-#pragma unroll 1
+    u32x4_t ao[MT];  // every row tile's o fragment requested up front (4 VGPRs a tile)
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+      ao[t] = __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(kOffOb),
+                                                    ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, PL_AUX);
+#pragma unroll  // (MT > 1: straight-line tiles, so the compiler's vmcnt counts stay exact across them)
     for (int t = 0; t < MT; ++t) {
-      const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(
-          rsrc_of(kOffOb), ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, PL_AUX);
+      const u32x4_t a = ao[t];
       f32x16_t acc32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
@@ -916,15 +986,21 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   {
     auto rsrc = rsrc_of(kOffXc);
     auto rsrc_f = rsrc_of(kOffFc);
-#pragma unroll 1
-    for (int t = 0; t < MT; ++t) {
-      u32x4_t ax[4][2];
+    u32x4_t ax[4][2], axn[4][2];  // this / the next row tile's A fragments (double-buffered, as phase A)
+    auto load_ax = [&](u32x4_t (&dst)[4][2], int t) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int hf = 0; hf < NHF; ++hf)
-          ax[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
+          dst[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
               rsrc, ((c * kMaxR + 32 * t + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
+    };
+    load_ax(ax, 0);
+    const int nfc = (32 * c + j) * 16 + (lane & 15);  // this lane's c_fc column (every row tile's)
+    const float fcu = Ly.fc_u[nfc], fcc = Ly.fc_c[nfc];
+#pragma unroll  // (MT > 1: straight-line tiles, so the compiler's vmcnt counts stay exact across them)
+    for (int t = 0; t < MT; ++t) {
+      if (MT > 1 && t + 1 < MT) load_ax(axn, t + 1);
       f32x4_t af[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
       float fs[2] = {0.f, 0.f}, fq[2] = {0.f, 0.f};
 #pragma unroll
@@ -956,18 +1032,29 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
 #pragma unroll
         for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
         const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
-        const int n = (32 * c + j) * 16 + (l & 15);
-        v = gelu_tanh_nc(fold_apply(v, rsd[rt], mu[rt], Ly.fc_u[n], Ly.fc_c[n]));
+        v = gelu_tanh_nc(fold_apply(v, rsd[rt], mu[rt], fcu, fcc));
         obf[rt * 16 + (l & 15)] = f2bf(v);
       }
       bar();
-      if (tid < 64) {  // [32 rows][16 columns] bf16 -> the cluster's f tile, write-through 16-B stores
+      if (MT > 1) {  // as phase A: the store issued by every wave, dropped (offset out of range) but in wave 0
+        const int rt = lane >> 1, half = lane & 1;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + rt * 16 + 8 * half);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, rsrc_of_lim(kOffFc), w == 0 ? ((c * kMaxR + 32 * t + rt) * 512 + 16 * j + 8 * half) * 2 : kDrop, 0,
+            PL_AUX);
+      } else if (tid < 64) {  // [32 rows][16 columns] bf16 -> the cluster's f tile, write-through 16-B stores
         const int rt = tid >> 1, half = tid & 1;
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + rt * 16 + 8 * half);
         __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_f, ((c * kMaxR + 32 * t + rt) * 512 + 16 * j + 8 * half) * 2,
                                                0, PL_AUX);
       }
-      if (MT > 1) bar();
+      if (MT > 1) {
+        bar();
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) ax[i][hf] = axn[i][hf];
+      }
     }
   }
   mark(10);
@@ -983,13 +1070,17 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   if (*abort_flag) return;
   {
     auto rsrc = rsrc_of(kOffFc);
-#pragma unroll 1
-    for (int t = 0; t < MT; ++t) {
-      u32x4_t a4[4];
+    u32x4_t a4[4], a4n[4];  // double-buffered over row tiles, as phase A
+    auto load_a4 = [&](u32x4_t (&dst)[4], int t) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        a4[i] = __builtin_amdgcn_raw_buffer_load_b128(
+        dst[i] = __builtin_amdgcn_raw_buffer_load_b128(
             rsrc, ((c * kMaxR + 32 * t + r32) * 512 + 16 * (w + 8 * i) + 8 * hb) * 2, 0, PL_AUX);
+    };
+    load_a4(a4, 0);
+#pragma unroll  // (MT > 1: straight-line tiles, so the compiler's vmcnt counts stay exact across them)
+    for (int t = 0; t < MT; ++t) {
+      if (MT > 1 && t + 1 < MT) load_a4(a4n, t + 1);
       f32x16_t acc32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc32[r] = 0.f;
@@ -1003,6 +1094,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       bar();
       store_partial(p2_(), t);
       bar();
+      if (MT > 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a4[i] = a4n[i];
+      }
     }
   }
   mark(12);
@@ -1237,6 +1332,7 @@ int launch_layers(const ItTsGptLayerW* const* lyw, const ItTsGptPlLayerW* const*
 int check_state(const ItTsGptDecodeState* st, void* scratch, const char* fn) {
   ITTS_REQUIRE(st->rows >= 1 && st->rows <= kMaxR, fn, "1..128 rows");
   ITTS_REQUIRE(!st->kv_rows || st->ld_rows >= st->max_kv, fn, "kv_rows [rows][ld_rows >= max_kv]");
+  ITTS_REQUIRE(!st->kv_rows || st->max_kv <= kKviMax, fn, "beam states: max_kv <= 3584 on the persistent path");
   ITTS_REQUIRE(st->x && st->xh && st->k_cache && st->v_cache && st->tstate, fn, "null state buffer");
   ITTS_REQUIRE((reinterpret_cast<uintptr_t>(scratch) & 255) == 0, fn, "scratch must be 256-B aligned");
   return 0;

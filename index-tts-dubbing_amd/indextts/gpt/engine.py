@@ -527,9 +527,12 @@ class HipGPT:
             _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
     # rows up to which a step runs on the persistent layers: one 32-row tile (C3 705.9 vs 761 us per step,
-    # C2 599 vs 613); at 96 rows (beam3) the launch chain is faster (1384 vs 1609 us, bench_r04e_b3.json
-    # vs bench_r04a_b3_pl0.json), so beams and the 128-row long-form chunks stay on the chain
+    # C2 599 vs 613); the 128-row long-form chunks stay on the chain.  Beam states (lineage table) up to
+    # PL_MAX_BEAM_ROWS: round 5 (row tiles straight-line with exact vmcnt counts, o prefetched, lineage indices
+    # in LDS) made beam3's 96-row step 1328-1336 us on the persistent layers vs 1359-1362 on the chain
+    # (profiles/r05_b3pl.sh r05u; round 4: 1609 vs 1384)
     PL_MAX_ROWS = int(os.environ.get("ITTS_PL_MAX_ROWS", "32"))
+    PL_MAX_BEAM_ROWS = int(os.environ.get("ITTS_PL_MAX_BEAM_ROWS", "96"))
 
     @property
     def pl_active(self):
@@ -551,7 +554,8 @@ class HipGPT:
         """persistent layers for this state: <= PL_MAX_ROWS (<= 128) rows, a 256-CU device with room for one
         workgroup per CU, not held off, and no other lane of this engine decoding concurrently (two
         persistent grids could each hold part of the CUs)"""
-        return (self.pl_active and st["B"] <= min(self.PL_MAX_ROWS, 128) and not st.get("multi_lane", False)
+        cap = max(self.PL_MAX_ROWS, self.PL_MAX_BEAM_ROWS) if st.get("kv_rows") is not None else self.PL_MAX_ROWS
+        return (self.pl_active and st["B"] <= min(cap, 128) and not st.get("multi_lane", False)
                 and bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), st["B"])))
 
     def pl_error(self):
