@@ -150,7 +150,9 @@ constexpr int64_t kOffP1 = kOffOb + (int64_t)kNC * kMaxR * 128 * 2;   // [8][128
 constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * kMaxR * kD * 4;    // [8][128][1024] bf16
 constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * kMaxR * kD * 2;    // [8][128][512] bf16
 constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * kMaxR * 512 * 2;   // [8][128][1024] f32
-constexpr int64_t kOffTrace = kOffP2 + (int64_t)kNC * kMaxR * kD * 4; // [256 WG][32] u64 (ITTS_PL_TRACE builds)
+constexpr int kPaStride = 72;                                         // floats per (head, group) partial
+constexpr int64_t kOffPa = kOffP2 + (int64_t)kNC * kMaxR * kD * 4;    // [16 heads][32 groups][72] f32 (SG)
+constexpr int64_t kOffTrace = kOffPa + (int64_t)kH * 32 * kPaStride * 4; // [256 WG][32] u64 (ITTS_PL_TRACE builds)
 constexpr int64_t kOffSeq = kOffTrace + (int64_t)kWG * 32 * 8;        // u32 epoch: launches since the reset
 constexpr int64_t kOffErr = kOffSeq + 256;                             // sticky error word
 constexpr int64_t kScratchBytes = kOffErr + 256;
@@ -264,7 +266,10 @@ __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uin
 // H16 (steps of at most 16 rows, MT = 1): the c_attn / c_fc phases load and multiply only the first 16-row
 // half of their A operands (rows 16-31 are padding: their outputs, never read, come out as the fold terms)
 // MULTI: the launch runs p.nl layers joined by the seam; else one layer (p.nl == 1), straight-line code
-template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false, bool H16 = false, bool MULTI = false>
+// SG (one-row steps, C2): the 32 softmax groups of each head spread over the cluster's 64 attention units (one
+// group each, every lane group of the unit computing the same one) instead of one unit per head; the groups'
+// (m, l, o) partials are merged in phase C in the in-unit merge's exact order (bit-identical)
+template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false, bool H16 = false, bool MULTI = false, bool SG = false>
 __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? kMaxLpl : 1> p) {
   static_assert(!H16 || MT == 1, "16-row halves: one row tile");
   constexpr int WAUX = WKEEP ? 0 : 2;  // LDS-DMA cache policy of the weight stream
@@ -341,6 +346,8 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   // attention: this workgroup's rows of head h are 32 pt + 2 jj + u (pass pt, unit u = waves 4u .. 4u+3)
   int u = w >> 2;
   int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
+  static_assert(!SG || (MT == 1 && H16 && !MULTI && !ROWS), "split groups: one-row small steps");
+  if constexpr (SG) g = 2 * jj + u;  // this unit's softmax group (keys g + 32 n of row 0)
   constexpr int NG = 32;
   u32x4_t kr[KB], vr[KB];
   // K/V rows of key index jk (0-based from the row's first valid key) of row `row`: the row's own cache
@@ -357,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk, jk)));
     }
   };
-  auto unit_row = [&](int pt) { return 32 * pt + 2 * jj + u; };
+  auto unit_row = [&](int pt) { return SG ? 0 : 32 * pt + 2 * jj + u; };
   // beams: this unit's lineage indices of row `row` (keys 0 .. nk-1) into LDS; every thread of the workgroup
   // calls it (it ends with the barrier the readers need)
   auto stage_kvi = [&](int row, int p0, int nk) __attribute__((always_inline)) {
@@ -814,11 +821,27 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       if constexpr (MULTI) __builtin_amdgcn_s_waitcnt(vm_wait_enc(ITTS_PL_KV_UNCOND && !H16 ? 2 * KB : 0));
       for (int j0 = NG * KB; j0 < nk; j0 += NG * KB) key_round(j0);
       if (pt == 0) mark(20);
+      if constexpr (SG) {
+        if (tu < 8) {  // lane group 0's copy of group g's partial -> [h][g]: o (64 f32), m, l (write-through)
+          const auto rp = rsrc_of(kOffPa);
+          const int base = ((h * 32 + g) * kPaStride) * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4_t{__float_as_uint(o8[0]), __float_as_uint(o8[1]), __float_as_uint(o8[2]), __float_as_uint(o8[3])},
+              rp, base + 32 * d8, 0, PL_AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4_t{__float_as_uint(o8[4]), __float_as_uint(o8[5]), __float_as_uint(o8[6]), __float_as_uint(o8[7])},
+              rp, base + 32 * d8 + 16, 0, PL_AUX);
+          if (d8 == 0)
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(m_run), __float_as_uint(l_run)}, rp,
+                                                  base + 256, 0, PL_AUX);
+        }
+      } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
-      if (d8 == 0) {
-        gm[g] = m_run;
-        gl[g] = l_run;
+        for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
+        if (d8 == 0) {
+          gm[g] = m_run;
+          gl[g] = l_run;
+        }
       }
     }
     // (after the block, not as its else: the structurizer turns an else into a DMA block ahead of the
@@ -830,6 +853,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       asm volatile("" : "+v"(idle)::"memory");
       if (idle) issue_dma(Ly);
     }
+    if constexpr (!SG) {
     bar();
     if (act_u) {
       const int dd = tu & (kHD - 1), qd = tu / kHD;
@@ -866,6 +890,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(kOffOb), ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, PL_AUX);
     }
+    }  // !SG
     if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
   mark(4);
@@ -919,10 +944,56 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   {
     const u32x4_t bb = *reinterpret_cast<const u32x4_t*>(lds_wo + w * 1024 + lane * 16);
     u32x4_t ao[MT];  // every row tile's o fragment requested up front (4 VGPRs a tile)
+    if constexpr (SG) {
+      // the cluster's two heads' 32 group partials -> LDS (red), then row 0's o from them in the in-unit merge's
+      // order: M = max m; per quarter of 8 groups L_q, a_q by fmaf in group order; L = sum L_q, a = sum a_q; o = a / L
+      const auto rp = rsrc_of(kOffPa);
+      constexpr int NV = 2 * 32 * kPaStride / 4, NPT = (NV + kThreads - 1) / kThreads;  // 16-B vectors
+      u32x4_t pt4[NPT];  // every load issued before the first LDS write (one round trip, not NPT)
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int v = tid + kThreads * k;
+        if (v < NV) pt4[k] = __builtin_amdgcn_raw_buffer_load_b128(rp, (2 * c * 32 * kPaStride) * 4 + 16 * v, 0, PL_AUX);
+      }
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int v = tid + kThreads * k;
+        if (v < NV) reinterpret_cast<u32x4_t*>(red)[v] = pt4[k];
+      }
+      bar();
+      u32x4_t a = u32x4_t{0u, 0u, 0u, 0u};
+      if (r32 == 0) {  // row 0 (the one row), this lane's 8 of the cluster's 128 dims
+        const int kk = 16 * w + 8 * hb, d0 = kk & (kHD - 1);
+        const float* P = red + (kk >> 6) * 32 * kPaStride;
+        float M = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) M = fmaxf(M, P[i * kPaStride + 64]);
+        float Ls = 0.f, at[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int qd = 0; qd < NQ; ++qd) {
+          float Lq = 0.f, aq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
+            const float wgt = __expf(P[i * kPaStride + 64] - M);
+            Lq = fmaf(P[i * kPaStride + 65], wgt, Lq);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) aq[e] = fmaf(P[i * kPaStride + d0 + e], wgt, aq[e]);
+          }
+          Ls += Lq;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) at[e] += aq[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = pack2bf(at[2 * e] / Ls, at[2 * e + 1] / Ls);
+      }
+      bar();  // red is the MFMA epilogue's next
+      ao[0] = a;
+    } else {
 #pragma unroll
     for (int t = 0; t < MT; ++t)
       ao[t] = __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(kOffOb),
                                                     ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, PL_AUX);
+    }
 #pragma unroll  // (MT > 1: straight-line tiles, so the compiler's vmcnt counts stay exact across them)
     for (int t = 0; t < MT; ++t) {
       const u32x4_t a = ao[t];
@@ -1203,7 +1274,9 @@ extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, true>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>),
                         reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKB, false, false, true>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, true>)};
+                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, true>),
+                        reinterpret_cast<const void*>(
+                            gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, false, kSmallH16>)};
     for (const void* k : ks) {
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess || nb < 1) occ = 0;
@@ -1244,6 +1317,16 @@ int layers_per_launch() {
     return v < 1 ? 1 : (v > kMaxLpl ? kMaxLpl : v);
   }();
   return n;
+}
+
+// one-row steps with the split softmax groups (SG, opt-in A/B: ITTS_PL_SPLITG=1); first measurement 613 vs
+// 500 us per C2 step (the phase-C staging of the 64 partials took one load round trip per 16-B vector, now one)
+bool split_groups() {
+  static const bool on = [] {
+    const char* e = getenv("ITTS_PL_SPLITG");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 
 PlLayerPtrs layer_ptrs(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl) {
@@ -1301,6 +1384,9 @@ int launch_layers(const ItTsGptLayerW* const* lyw, const ItTsGptPlLayerW* const*
     if (nl > 1)
       hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, true>), dim3(kWG), dim3(kThreads), 0,
                          s, a);
+    else if (st->rows == 1 && kSmallH16 && split_groups())
+      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, false, kSmallH16>), dim3(kWG),
+                         dim3(kThreads), 0, s, a1);
     else if (keep)
       hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, true, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s, a1);
     else
