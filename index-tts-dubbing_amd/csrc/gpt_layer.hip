@@ -1319,8 +1319,10 @@ int layers_per_launch() {
   return n;
 }
 
-// one-row steps with the split softmax groups (SG, opt-in A/B: ITTS_PL_SPLITG=1); first measurement 613 vs
-// 500 us per C2 step (the phase-C staging of the 64 partials took one load round trip per 16-B vector, now one)
+// one-row steps with the split softmax groups (SG, opt-in A/B: ITTS_PL_SPLITG=1): bit-identical, measured slower,
+// C2 step 604 vs 500 us (profiles/pl_trace_r05x_sg{0,1}.txt): the attention ends ~2 us earlier, but the E2 drain then
+// waits for the layer's weight DMA (no long attention to hide it any more) and phase C's serial 32-group merge in
+// 16 lanes takes 4.2 us
 bool split_groups() {
   static const bool on = [] {
     const char* e = getenv("ITTS_PL_SPLITG");
