@@ -364,7 +364,11 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk, jk)));
     }
   };
-  auto unit_row = [&](int pt) { return SG ? 0 : 32 * pt + 2 * jj + u; };
+  // beams (ROWS) with whole row tiles: unit (jj, u) takes rows MT (2 jj + u) + pt, i.e. one utterance's beams when
+  // it has MT of them (beam3: 96 rows, 3 passes), so the lineage rows its beams share are re-read by the same CU in
+  // consecutive passes (L2 / Infinity Cache) instead of by three CUs on different XCDs
+  const bool beam_major = ROWS && MT > 1 && R == 32 * MT;
+  auto unit_row = [&](int pt) { return SG ? 0 : beam_major ? MT * (2 * jj + u) + pt : 32 * pt + 2 * jj + u; };
   // beams: this unit's lineage indices of row `row` (keys 0 .. nk-1) into LDS; every thread of the workgroup
   // calls it (it ends with the barrier the readers need)
   auto stage_kvi = [&](int row, int p0, int nk) __attribute__((always_inline)) {
