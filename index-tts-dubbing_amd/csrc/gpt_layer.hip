@@ -128,6 +128,18 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 #ifndef ITTS_PL_KV_LATE
 #define ITTS_PL_KV_LATE 0
 #endif
+// A/B switches measured neutral or slower (profiles/r05_xc16.sh, r05xa_ab.txt), off by default:
+//   ITTS_PL_XC16=1: phase D's x1^ copies as 16-B write-through stores (4 lanes gathered by shuffles): C3 643.3 /
+//     641.8 vs 640.6 / 642.4 us per step, C2 500.7 / 501.1 vs 499.8 / 499.3
+//   ITTS_PL_BEAM_MAJOR=1: beam lineage rows, one attention unit takes an utterance's MT beams (one pass reads
+//     the shared lineage rows): beam3 1422 / 1426 vs 1334 / 1330 us -- a unit's first pass then needs rows of
+//     every row tile, so no attention pass starts before phase A's last row tile has landed
+#ifndef ITTS_PL_XC16
+#define ITTS_PL_XC16 0
+#endif
+#ifndef ITTS_PL_BEAM_MAJOR
+#define ITTS_PL_BEAM_MAJOR 0
+#endif
 #ifndef ITTS_PL_DMA_EARLY
 #define ITTS_PL_DMA_EARLY 0
 #endif
@@ -367,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   // beams (ROWS) with whole row tiles: unit (jj, u) takes rows MT (2 jj + u) + pt, i.e. one utterance's beams when
   // it has MT of them (beam3: 96 rows, 3 passes), so the lineage rows its beams share are re-read by the same CU in
   // consecutive passes (L2 / Infinity Cache) instead of by three CUs on different XCDs
-  const bool beam_major = ROWS && MT > 1 && R == 32 * MT;
+  const bool beam_major = ITTS_PL_BEAM_MAJOR && ROWS && MT > 1 && R == 32 * MT;
   auto unit_row = [&](int pt) { return SG ? 0 : beam_major ? MT * (2 * jj + u) + pt : 32 * pt + 2 * jj + u; };
   // beams: this unit's lineage indices of row `row` (keys 0 .. nk-1) into LDS; every thread of the workgroup
   // calls it (it ends with the barrier the readers need)
@@ -1039,8 +1051,15 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       }
       const float2 xo = row < R ? x_raw[t] : float2{0.f, 0.f};
       x1[t] = float2{xo.x + pp.x, xo.y + pp.y};
-      st_sc1_u32(reinterpret_cast<uint32_t*>(xc() + (((int64_t)c * kMaxR + row) * kD + xcol) * 2),
-                 pack2bf(x1[t].x, x1[t].y));
+      const uint32_t pk = pack2bf(x1[t].x, x1[t].y);
+      if (ITTS_PL_XC16) {  // 8 columns (4 lanes) per 16-B write-through store (a 4-B sc1 store is one fabric write)
+        const uint32_t n1 = __shfl_down(pk, 1, 64), n2 = __shfl_down(pk, 2, 64), n3 = __shfl_down(pk, 3, 64);
+        if ((lane & 3) == 0)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{pk, n1, n2, n3}, rsrc_of(kOffXc),
+                                                 ((c * kMaxR + row) * kD + xcol) * 2, 0, PL_AUX);
+      } else {
+        st_sc1_u32(reinterpret_cast<uint32_t*>(xc() + (((int64_t)c * kMaxR + row) * kD + xcol) * 2), pk);
+      }
     }
   }
   mark(8);

@@ -558,6 +558,16 @@ class HipGPT:
         return (self.pl_active and st["B"] <= min(cap, 128) and not st.get("multi_lane", False)
                 and bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), st["B"])))
 
+    def pl_takes(self, rows: int, beams: bool = False) -> bool:
+        """would a decode of ``rows`` rows (beam states: utterances x num_beams) run on the persistent layers
+        (no lane split, within the row cap, supported on this device)"""
+        cap = max(self.PL_MAX_ROWS, self.PL_MAX_BEAM_ROWS) if beams else self.PL_MAX_ROWS
+        if not (self.pl_active and 0 < rows <= min(cap, 128)):
+            return False
+        if not beams and len(self._lane_bounds(rows, None)) > 1:
+            return False
+        return bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), rows))
+
     def pl_error(self):
         """hand-off timeout code recorded by the persistent layers (0 = none); syncs the stream."""
         if not self.pl:

@@ -43,10 +43,13 @@ def test_synthesize_is_deterministic(tts):
     _same(r1, r2)
 
 
-def test_synthesize_many_equals_synthesize(tts):
+@pytest.mark.parametrize("overlap", [None, True, False])
+def test_synthesize_many_equals_synthesize(tts, overlap):
+    """auto (5-row batches: every decode fits the persistent layers -> back to back on one stream), forced
+    overlap (decode on the launch chain beside the back stream) and forced serial: all equal synthesize"""
     batches = [_inputs(tts.cfg, 5, s) for s in (2, 3, 4)]
     want = [tts.synthesize(m, t, max_mel_tokens=24) for m, t in batches]
-    got = tts.synthesize_many(batches, max_mel_tokens=24)
+    got = tts.synthesize_many(batches, max_mel_tokens=24, overlap=overlap)
     torch.cuda.synchronize()
     for w, g in zip(want, got):
         _same(w, g)

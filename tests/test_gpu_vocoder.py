@@ -135,6 +135,34 @@ def test_activation_kernel_c96_whole_row_jobs_equal_block_jobs(monkeypatch):
     assert bad.numel() == 0, (bad[:8].tolist(), lens.tolist())
 
 
+@pytest.mark.parametrize("C", [24, 32, 48, 96, 128])
+def test_activation_kernel_16b_stores_equal_8b_stores(monkeypatch, C):
+    """Interior outputs leave as 16-B stores (lanes n and n + 32 swap channel halves, ITTS_ACT_ST16=1) or as
+    the accumulator's 8-B quarters (default): the same values in the same places, ragged lengths included
+    (every channel-block count: NB = 1, 2, 3, 4)."""
+    from indextts.utils.synthetic import kaiser_sinc_lowpass
+    _hip, lib = _lib()
+    B, T = 12, 1100
+    g = torch.Generator().manual_seed(C + 7)
+    lens = torch.randint(1, T + 1, (B,), generator=g, dtype=torch.int32)
+    lens[0], lens[1], lens[2] = T, 1, 5
+    x = (torch.randn(B, T, C, generator=g) * 1.5).to(torch.bfloat16).cuda()
+    f = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).cuda()
+    la, lb = (torch.randn(C, generator=g) * 0.5).cuda(), (torch.randn(C, generator=g) * 0.5).cuda()
+    lensd = lens.cuda()
+    out = []
+    for st16 in ("1", "0"):
+        monkeypatch.setenv("ITTS_ACT_ST16", st16)
+        y = torch.full((B, T, C), -12352.0, dtype=torch.bfloat16, device="cuda")
+        _hip.check(lib.itts_aa_snakebeta_fwd(x.data_ptr(), y.data_ptr(), f.data_ptr(), f.data_ptr(), la.data_ptr(),
+                                             lb.data_ptr(), lensd.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1,
+                                             _hip.BF16, _hip.BF16, _hip.stream_ptr()), "fwd")
+        torch.cuda.synchronize()
+        out.append(y.view(torch.int16).cpu())
+    bad = (out[0] != out[1]).nonzero()
+    assert bad.numel() == 0, (bad[:8].tolist(), lens.tolist())
+
+
 @pytest.mark.parametrize("C,B,T", [(24, 160, 3000), (768, 64, 700), (192, 48, 1500), (96, 24, 2100)])
 def test_activation_kernel_mfma_persistent_many_jobs(C, B, T):
     """The MFMA activation kernel is persistent (each workgroup walks several (utterance, time tile)
