@@ -526,12 +526,14 @@ class HipGPT:
             self._beam_step(st, 1)
             _hip.check(self.lib.itts_step_advance(st["t"].data_ptr(), 1, stream), "itts_step_advance")
 
-    # rows up to which a step runs on the persistent layers: one 32-row tile (C3 705.9 vs 761 us per step,
-    # C2 599 vs 613); the 128-row long-form chunks stay on the chain.  Beam states (lineage table) up to
-    # PL_MAX_BEAM_ROWS: round 5 (row tiles straight-line with exact vmcnt counts, o prefetched, lineage indices
-    # in LDS) made beam3's 96-row step 1328-1336 us on the persistent layers vs 1359-1362 on the chain
-    # (profiles/r05_b3pl.sh r05u; round 4: 1609 vs 1384)
-    PL_MAX_ROWS = int(os.environ.get("ITTS_PL_MAX_ROWS", "32"))
+    # rows up to which a step runs on the persistent layers: every shape the kernel supports (<= 128 rows, four
+    # row tiles).  Round 5 (row tiles straight-line with exact vmcnt counts, o prefetched) made the multi-tile
+    # steps faster than the chain too: greedy 32 / 64 / 96 / 128 rows 664 / 1016 / 1330 / 1649 us per step vs
+    # 780 / 1127 / 1452 / 1688 on the chain (profiles/ubench_pl_rows.py, pl_rows_r05rows.txt), and the C5
+    # long-form 128-row chunks 1794 / 1829 vs 1784 / 1777 audio-s/s run back to back on them (r05c5_ab.txt;
+    # round 4 kept them on the chain, 32 rows was the break-even then).  Beam states (lineage table) up to
+    # PL_MAX_BEAM_ROWS: beam3's 96-row step 1330 us vs 1360 on the chain (profiles/r05_b3pl.sh r05u)
+    PL_MAX_ROWS = int(os.environ.get("ITTS_PL_MAX_ROWS", "128"))
     PL_MAX_BEAM_ROWS = int(os.environ.get("ITTS_PL_MAX_BEAM_ROWS", "96"))
 
     @property

@@ -5,7 +5,7 @@ every teacher-forced step and the chosen ids -- at 32 rows (C3), 1 row (C2), 128
 chunks, 4 row tiles), ragged 7- and 45-row batches with left padding, and beam search / beam sample
 (96 rows through the KV lineage table), with keys from the prompt block up to KV length ~160.  Parity of the chain
 itself with the reference is tests/test_gpu_fullsize.py (which runs on whichever path the engine
-picks: the persistent one for <= 32 rows).
+picks: the persistent one for <= 128 rows).
 
 Round 5: the same bit identity at the bench's own decode shape (C3: L = 48 text ids, 400 steps, keys up to
 483: four 128-key rounds, the peeled round 0 and the full-depth key loop) at B = 32 and B = 1; lane reuse
@@ -232,8 +232,9 @@ def test_synthesize_many_tail_chunk_beside_back_stream():
     want = []
     for m, t in batches:
         want.append(tts.synthesize(m, t, max_mel_tokens=24, min_new_tokens=24))
-        assert tts.gpt._pl_ran == (len(t) <= 32)
-    got = tts.synthesize_many(batches, max_mel_tokens=24, min_new_tokens=24)
+        assert tts.gpt._pl_ran == tts.gpt.pl_takes(len(t))
+    # overlap forced: auto would run these batches back to back when every chunk fits the persistent layers
+    got = tts.synthesize_many(batches, max_mel_tokens=24, min_new_tokens=24, overlap=True)
     torch.cuda.synchronize()
     assert not tts.gpt._pl_ran  # the tail chunk beside the back stream: launch chain
     assert tts.gpt.pl_error() == 0
