@@ -97,7 +97,7 @@ class IndexTTS:
     # long-form chunks (infer_many, the cue lookahead): the decode step is latency-bound at 32 rows, so
     # more rows per step raise throughput -- 128 rows decode at 194 ms per 32 rows of 400 codes vs 330
     # for 32 rows alone (profiles/lanes_probe_r02.txt); per-row results do not depend on the chunking
-    LONGFORM_BATCH = 128
+    LONGFORM_BATCH = int(os.environ.get("ITTS_LONGFORM_BATCH", "128"))
 
     def __init__(self, cfg_path="checkpoints/config.yaml", model_dir="checkpoints", is_fp16=True, device=None,
                  use_cuda_kernel=None):
