@@ -381,6 +381,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   // consecutive passes (L2 / Infinity Cache) instead of by three CUs on different XCDs
   const bool beam_major = ITTS_PL_BEAM_MAJOR && ROWS && MT > 1 && R == 32 * MT;
   auto unit_row = [&](int pt) { return SG ? 0 : beam_major ? MT * (2 * jj + u) + pt : 32 * pt + 2 * jj + u; };
+  // phase A's row tiles gather in the same order: tile t = rows MT i + t (beam t of every utterance), so attention
+  // pass pt needs only tile pt's q/k/v and the tiles keep overlapping the passes (row-independent arithmetic:
+  // every row's c_attn output is the same in any tile)
+  auto a_row = [&](int t, int i) { return beam_major ? MT * i + t : 32 * t + i; };
   // beams: this unit's lineage indices of row `row` (keys 0 .. nk-1) into LDS; every thread of the workgroup
   // calls it (it ends with the barrier the readers need)
   auto stage_kvi = [&](int row, int p0, int nk) __attribute__((always_inline)) {
@@ -472,7 +476,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
         bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
 #pragma unroll
       for (int t = 0; t < NHF; ++t)
-        av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
+        av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)a_row(0, 16 * t + c16) * kD + 32 * s + 8 * q4);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (!ITTS_PL_KV_LATE) kv_round0(p.kc, p.vc);
@@ -564,7 +568,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
 #pragma unroll
       for (int t = 0; t < NHF; ++t)
         av[i][t] = __builtin_amdgcn_raw_buffer_load_b128(
-            rsrc_xh(), ((16 * t + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
+            rsrc_xh(), (a_row(0, 16 * t + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
   }
   mark(1);
   dbg(0, (uint32_t)kidx);
@@ -597,7 +601,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
           avn[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
-              rsrc_xh(), ((32 * (t + 1) + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
+              rsrc_xh(), (a_row(t + 1, 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
     }
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
     float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
@@ -636,7 +640,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       float v = 0.f;
 #pragma unroll
       for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
-      const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = 32 * t + rt;
+      const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = a_row(t, rt);
       v = fold_apply(v, rsd[rt], mu[rt], uc0, uc1);
       const int i = kQC * jj + cq;
       const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
