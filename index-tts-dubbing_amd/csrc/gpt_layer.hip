@@ -131,9 +131,10 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 // A/B switches measured neutral or slower (profiles/r05_xc16.sh, r05xa_ab.txt), off by default:
 //   ITTS_PL_XC16=1: phase D's x1^ copies as 16-B write-through stores (4 lanes gathered by shuffles): C3 643.3 /
 //     641.8 vs 640.6 / 642.4 us per step, C2 500.7 / 501.1 vs 499.8 / 499.3
-//   ITTS_PL_BEAM_MAJOR=1: beam lineage rows, one attention unit takes an utterance's MT beams (one pass reads
-//     the shared lineage rows): beam3 1422 / 1426 vs 1334 / 1330 us -- a unit's first pass then needs rows of
-//     every row tile, so no attention pass starts before phase A's last row tile has landed
+//   ITTS_PL_BEAM_MAJOR=1: beam lineage rows, one attention unit takes an utterance's MT beams in consecutive
+//     passes (phase A's row tiles gathered to match): beam3 1422 / 1426 vs 1334 / 1330 us -- in the default order
+//     an utterance's beams are three units of one cluster reading the same lineage rows at once (one XCD's L2);
+//     a pass apart (~8 MB of K/V per cluster) they miss the 4 MB L2
 #ifndef ITTS_PL_XC16
 #define ITTS_PL_XC16 0
 #endif
@@ -376,9 +377,9 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk, jk)));
     }
   };
-  // beams (ROWS) with whole row tiles: unit (jj, u) takes rows MT (2 jj + u) + pt, i.e. one utterance's beams when
-  // it has MT of them (beam3: 96 rows, 3 passes), so the lineage rows its beams share are re-read by the same CU in
-  // consecutive passes (L2 / Infinity Cache) instead of by three CUs on different XCDs
+  // ITTS_PL_BEAM_MAJOR=1, beams (ROWS) with whole row tiles: unit (jj, u) takes rows MT (2 jj + u) + pt, i.e. one
+  // utterance's beams in consecutive passes (slower, see the switch: the default order has them on three units of
+  // the cluster at once, sharing the lineage rows through the XCD's L2)
   const bool beam_major = ITTS_PL_BEAM_MAJOR && ROWS && MT > 1 && R == 32 * MT;
   auto unit_row = [&](int pt) { return SG ? 0 : beam_major ? MT * (2 * jj + u) + pt : 32 * pt + 2 * jj + u; };
   // phase A's row tiles gather in the same order: tile t = rows MT i + t (beam t of every utterance), so attention
