@@ -40,10 +40,10 @@ PEAK_HBM_GBS = 8000.0
 # per decoding and decode path (persistent layers or the launch chain): None until measured for this build
 # PMC files are measured on the C3 workload (profiles/pmc_decode.py, pmc_vocoder.py): other workloads report
 # traffic null rather than C3's bytes
-TRAFFIC_DECODE = {("c3", "greedy", True): "traffic_decode_pl_r05z.json", ("c3", "greedy", False): "traffic_decode_r04.json",
-                  ("c3", "beam3", True): "traffic_decode_beam3_r05z.json",
+TRAFFIC_DECODE = {("c3", "greedy", True): "traffic_decode_pl_r05zh.json", ("c3", "greedy", False): "traffic_decode_r04.json",
+                  ("c3", "beam3", True): "traffic_decode_beam3_r05zh.json",
                   ("c3", "beam3", False): "traffic_decode_beam3_r05f.json"}
-TRAFFIC_VOCODER = {"c3": "traffic_vocoder_r05z.json"}
+TRAFFIC_VOCODER = {"c3": "traffic_vocoder_r05zh.json"}
 
 
 class KernelTimer:
