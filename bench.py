@@ -90,13 +90,12 @@ def install_conv_timer(voc, timer):
     voc._conv = timed
 
 
-def install_hbm_timers(voc, t_act, t_amp, t_ampact=None):
-    """HIP events around the standalone activation launches, the AMPBlock1 conv launches
-    (itts_amp_conv_fwd, C = 24 / 48 / 96, conv-only or with the activation fused) and the fused
-    conv1 -> act2 launches (itts_amp_conv_act_fwd, C = 24 / 48), with their algorithmic HBM bytes: valid
-    rows x channels, each element read once and written once (+ residual rows read; + the packed
+def install_hbm_timers(voc, t_act, t_amp):
+    """HIP events around the standalone activation launches and the AMPBlock1 conv launches
+    (itts_amp_conv_fwd, C = 24 / 48 / 96, conv-only or with the activation fused), with their algorithmic HBM
+    bytes: valid rows x channels, each element read once and written once (+ residual rows read; + the packed
     weights once)."""
-    orig_act, orig_amp, orig_ampact = voc._act, voc._amp, voc._amp_act
+    orig_act, orig_amp = voc._act, voc._amp
 
     def act(a, x, y, lens):
         nbytes = 2.0 * voc.rows * x.shape[2] * 2
@@ -108,13 +107,7 @@ def install_hbm_timers(voc, t_act, t_amp, t_ampact=None):
         return t_amp.wrap(lambda: orig_amp(c, x, y, lens, a, r1, r2, alpha), 2.0 * voc.rows * c.cout * c.cin * c.ntaps,
                           nbytes)
 
-    def amp_act(c, x, y, lens, a):
-        nbytes = 2.0 * voc.rows * (c.cin + c.cout) + 2.0 * c.ntaps * c.cin * c.cout
-        if t_ampact is None:
-            return orig_ampact(c, x, y, lens, a)
-        return t_ampact.wrap(lambda: orig_ampact(c, x, y, lens, a), 2.0 * voc.rows * c.cout * c.cin * c.ntaps, nbytes)
-
-    voc._act, voc._amp, voc._amp_act = act, amp, amp_act
+    voc._act, voc._amp = act, amp
 
 
 def _traffic(name, key):
@@ -278,9 +271,9 @@ def main():
         args.batch = 1
     B, N, L = args.batch, args.codes, args.text_len
     tts = BatchedTTS(gsd, vsd, cfg, dev, "bf16", max_kv=32 + L + 2 + 1 + N + 8)
-    timer, t_act, t_amp, t_ampact = KernelTimer(), KernelTimer(), KernelTimer(), KernelTimer()
+    timer, t_act, t_amp = KernelTimer(), KernelTimer(), KernelTimer()
     install_conv_timer(tts.vocoder, timer)
-    install_hbm_timers(tts.vocoder, t_act, t_amp, t_ampact)
+    install_hbm_timers(tts.vocoder, t_act, t_amp)
     # global batch of B * world utterances; utterance i runs on rank i % world (weak scaling)
     mels, texts = make_inputs(cfg, shard(B * world, world, rank), L, args.prompt_frames)
     mels = [m.to(dev) for m in mels]
@@ -331,10 +324,10 @@ def main():
         # launches are timed one by one in an extra, untimed step through the Python launch sequence
         # (the same kernels, HipBigVGAN._forward_py)
         tts.vocoder.cforward = False
-        timer.enabled = t_act.enabled = t_amp.enabled = t_ampact.enabled = True
+        timer.enabled = t_act.enabled = t_amp.enabled = True
         step()
         torch.cuda.synchronize()
-        timer.enabled = t_act.enabled = t_amp.enabled = t_ampact.enabled = False
+        timer.enabled = t_act.enabled = t_amp.enabled = False
         tts.vocoder.cforward = True
     k_ms, k_flops, k_n = timer.result()
     dec = None
@@ -382,9 +375,7 @@ def main():
     for key, t, name, tkey in (("roofline_vocoder_act", t_act, "itts_aa_snakebeta_fwd (Activation1d, every AMP "
                                 "stage and activation_post)", "aa_snakebeta_bytes_per_launch"),
                                ("roofline_vocoder_amp", t_amp, "itts_amp_conv_fwd (AMPBlock1 dilated convs "
-                                "+ residuals, C = 24 / 48 / 96)", "amp_conv_bytes_per_launch"),
-                               ("roofline_vocoder_amp_act", t_ampact, "itts_amp_conv_act_fwd (AMPBlock1 conv1 -> "
-                                "act2 in one launch, C = 24 / 48)", "amp_conv_act_bytes_per_launch")):
+                                "+ residuals, C = 24 / 48 / 96)", "amp_conv_bytes_per_launch")):
         ms, _, n = t.result()
         if n:
             gbs = t.bytes / (ms * 1e-3) / 1e9

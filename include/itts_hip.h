@@ -90,20 +90,19 @@ int itts_amp_conv_fwd(const void* x, int64_t x_sb, int64_t ldx, const float* up1
                       const void* r1, const void* r2, void* y, int64_t y_sb, int64_t ldy, const int32_t* lengths,
                       int B, int Tmax, int Cin, int Cout, int ntaps, const int32_t* tap_off, float alpha,
                       void* stream);
-/* conv1 -> act2 of an AMPBlock1 layer (models.py:65-74) in one launch, the narrow stages (Cin = Cout = 24 or 48):
- *   y[b][t][:] = Activation1d(conv(x) + bias)[b][t][:]   (up12 / down12 / log_alpha / log_beta: act2's)
- * with x rows outside [0, lengths[b]) the conv's zero padding and the activation's replicate padding at the
- * utterance edges -- bit-identical to itts_amp_conv_fwd (no residuals, alpha 1) followed by
- * itts_aa_snakebeta_fwd on its bf16 output, without that output's HBM round trip.  bf16 channel-last. */
-int itts_amp_conv_act_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, const float* bias, void* y,
-                          int64_t y_sb, int64_t ldy, const int32_t* lengths, int B, int Tmax, int Cin, int Cout,
-                          int ntaps, const int32_t* tap_off, const float* up12, const float* down12,
-                          const float* log_alpha, const float* log_beta, void* stream);
 /* conv_post (Conv1d(C->1, K, pad K/2), bias) + tanh (models.py:246-248), optionally also the int16
  * PCM of infer.py:627,653 (clamp(32767*wav, +-32767) truncated toward zero, quirk Q8). */
 int itts_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* w, float bias, int C, int K,
                         const int32_t* lengths, int B, int Tmax, float* wav, int16_t* pcm, int64_t y_sb,
                         int dtype_in, void* stream);
+/* activation_post (Activation1d, models.py:245; filters / log_alpha / log_beta as itts_aa_snakebeta_fwd) fused in
+ * front of conv_post + tanh (+ int16): bf16 channel-last x, C a multiple of 8 and at most 32, K odd <= 15.  The
+ * activation output never leaves the chip; results bit-identical to itts_aa_snakebeta_fwd (bf16) followed by
+ * itts_conv_post_tanh on its output. */
+int itts_act_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* up12, const float* down12,
+                            const float* log_alpha, const float* log_beta, const float* w, float bias, int C, int K,
+                            const int32_t* lengths, int B, int Tmax, float* wav, int16_t* pcm, int64_t y_sb,
+                            void* stream);
 
 /* The whole generator (BigVGAN.forward, models.py:201-250, + the int16 conversion of infer.py:627-631)
  * as one call.  Weights in the packings above: every conv as an igemm-packed tap list. */
@@ -133,8 +132,7 @@ typedef struct ItTsBigvganStage {
   int n_blocks, n_layers;      /* resblocks (kernel sizes) x dilations */
   const ItTsAmpLayer* layers;  /* [n_blocks][n_layers] */
   int amp_mode;                /* 0: act kernel + implicit-GEMM conv; 1: act fused into itts_amp_conv_fwd;
-                                  2: act kernel + itts_amp_conv_fwd without activation; 3: act kernel +
-                                  itts_amp_conv_act_fwd (conv1 -> act2) + itts_amp_conv_fwd (conv2) */
+                                  2: act kernel + itts_amp_conv_fwd without activation */
 } ItTsBigvganStage;
 typedef struct ItTsBigvganWeights {
   int n_stages, gpt_dim, spk_dim;

@@ -188,15 +188,9 @@ __global__ __launch_bounds__(kThreads) void aa_snakebeta_kernel(ActArgs p) {
 #ifndef ITTS_ACT_TAPS_LDS  // the FIR operands in LDS instead of 56 VGPRs per lane
 #define ITTS_ACT_TAPS_LDS 0  // measured neutral (profiles/ubench_act_r03.txt): the taps are not what holds the registers
 #endif
-// ITTS_ACT_ST16=1: interior outputs as 16-B stores (lane pairs swap channel halves) instead of the accumulator's
-// 8-B quarters; bit-identical, measured neutral (vocoder 87.6 / 88.0 / 87.4 ms vs 87.7 / 87.2 / 87.0 at the C3
-// shape, profiles/r05xa_ab.txt), so off by default; read per launch (the bit-identity test toggles it)
-bool act_st16_enabled() {
-  const char* e = getenv("ITTS_ACT_ST16");
-  return e && e[0] == '1';
-}
-
-template <int NB, int S, bool V16>
+// (16-B interior stores, lane pairs swapping channel halves, were bit-identical and measured neutral -- vocoder
+// 87.6 / 88.0 / 87.4 ms vs 87.7 / 87.2 / 87.0, profiles/r05xa_ab.txt -- and removed in round 6)
+template <int NB, int S>
 #ifndef ITTS_ACT_WPS  // waves per SIMD the register allocation targets
 #define ITTS_ACT_WPS 2  // 3 spills 32-37 VGPRs: 30-40 % slower (profiles/ubench_act_r03.txt)
 #endif
@@ -267,31 +261,6 @@ __global__ __launch_bounds__(256, ITTS_ACT_WPS) void aa_snake_mfma_kernel(ActArg
     const int ntile = sidx < NS ? min(S, max(0, (len - ts + 31) / 32)) : 0;
     itts_actm::strip<PX>(win, sidx * 32 * S, cb, ntile, T, a_rev, inv_b, [&](int i, const f32x16_t& acc) {
       const int t = ts + 32 * i + (lane & 31);
-      if constexpr (V16) {
-        // lanes n and n + 32 (same time, channel halves 4h .. 4h+3 of every 8) swap halves so that each
-        // writes two whole 8-channel groups: h = 0 groups 0 and 2, h = 1 groups 1 and 3, 16 B a store
-        uint32_t mine[4], give[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          mine[g] = pack2bf(acc[4 * g], acc[4 * g + 1]);
-          give[g] = pack2bf(acc[4 * g + 2], acc[4 * g + 3]);
-        }
-        // send what the partner keeps: h = 0 sends groups 1, 3; h = 1 sends groups 0, 2
-        const uint32_t s0 = h ? mine[0] : mine[1], s1 = h ? give[0] : give[1];
-        const uint32_t s2 = h ? mine[2] : mine[3], s3 = h ? give[2] : give[3];
-        const uint32_t r0 = __shfl_xor(s0, 32, 64), r1 = __shfl_xor(s1, 32, 64);
-        const uint32_t r2 = __shfl_xor(s2, 32, 64), r3 = __shfl_xor(s3, 32, 64);
-        if (t < 3 || t >= len - 3) return;  // edges: VALU fix-up below (both lanes of a pair agree)
-        uint16_t* yr = y + (int64_t)t * p.syt + c0 + cb;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int g = 2 * k + h;
-          const u32x4_t o = h ? u32x4_t{k ? r2 : r0, k ? r3 : r1, mine[g], give[g]}
-                              : u32x4_t{mine[g], give[g], k ? r2 : r0, k ? r3 : r1};
-          if (c0 + cb + 8 * g < p.C) *reinterpret_cast<u32x4_t*>(yr + 8 * g) = o;
-        }
-        return;
-      }
       if (t < 3 || t >= len - 3) return;  // edges: VALU fix-up below
       uint16_t* yr = y + (int64_t)t * p.syt + c0 + cb + 4 * h;
 #pragma unroll
@@ -326,19 +295,13 @@ __global__ __launch_bounds__(256, ITTS_ACT_WPS) void aa_snake_mfma_kernel(ActArg
 #endif
 template <int NB, int S>
 void launch_mfma(const ActArgs& a, hipStream_t s) {
-  // 16-B output stores need whole 8-channel groups and 16-B aligned rows
-  const bool v16 = act_st16_enabled() && a.C % 8 == 0 && a.syt % 8 == 0 && a.syb % 8 == 0 &&
-                   (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
   constexpr int TT = (4 / NB) * 32 * S;
   const int nblk = (a.C + 31) / 32, ngrp = (nblk + NB - 1) / NB;
   const int ntt = (a.T + TT - 1) / TT, njobs = ntt * a.B;
   int per = ITTS_ACT_WGS / ngrp;
   per = per < 1 ? 1 : (per > njobs ? njobs : per);
   const size_t lds = (size_t)(TT + 32) * NB * 64 + 128 + (ITTS_ACT_TAPS_LDS ? itts_actm::kTapsLdsBytes : 0);
-  if (v16)
-    hipLaunchKernelGGL((aa_snake_mfma_kernel<NB, S, true>), dim3(ngrp, per, 1), dim3(256), lds, s, a, ntt, njobs);
-  else
-    hipLaunchKernelGGL((aa_snake_mfma_kernel<NB, S, false>), dim3(ngrp, per, 1), dim3(256), lds, s, a, ntt, njobs);
+  hipLaunchKernelGGL((aa_snake_mfma_kernel<NB, S>), dim3(ngrp, per, 1), dim3(256), lds, s, a, ntt, njobs);
 }
 
 template <typename TI, typename TO>

@@ -52,7 +52,6 @@ struct AcArgs {
   const uint16_t* x;
   int64_t sxb, ldx;
   const float *up, *down, *log_alpha, *log_beta;  // log_alpha == nullptr: no activation
-  const float *pup, *pdown, *plog_alpha, *plog_beta;  // EPI: the activation applied to the conv output
   const uint16_t* w;
   const float* bias;
   const uint16_t* r1;
@@ -76,156 +75,22 @@ __device__ __forceinline__ float ld_bf(const uint16_t* p) { return __uint_as_flo
 // CK: the channel count (Cin == Cout) as a compile-time constant for the BigVGAN stages, 0 = runtime
 // CIN_PAD: the K extent staged and multiplied (a multiple of 16 >= Cin); the packed weights' rows
 // are WS = CIN_PAD rounded up to 32 wide (the igemm packing)
-// The EPI epilogue: conv accumulators (+ bias) -> bf16 activation window in LDS (act_mfma.h layout, row r =
-// time t_out - 7 + r) -> the activation's strips -> y.  Window rows 1 .. TO + 12 carry the conv output at
-// their (replicate-clamped) times, every other row is zero: the same window aa_snake_mfma_kernel loads.
-// LDS byte offset of the EPI activation's 24 taps: past both the conv's LDS and the activation window, so
-// they are stored once at the start (with the other per-launch constants, whose loads are issued beside the
-// window's instead of in the epilogue's dependency chain)
-template <int CI, int CO, int TT>
-constexpr int epi_tl_off() {
-  constexpr int conv = (TT + kSpan) * (CI * 2 + 16) + 2 * CO * (CI * 2 + 16);
-  constexpr int actw = TT * (CO / 32) * 64;
-  return ((conv > actw ? conv : actw) + 15) / 16 * 16;
-}
-// the wave's activation strip in the EPI epilogue: 32-channel block blk, output tiles [tile0, tile1)
-template <int COUT_PAD, int TT>
-struct EpiStrips {
-  static constexpr int NB = COUT_PAD / 32, NTO = (TT - 32) / 32, SPB = NB >= 4 ? 1 : 4 / NB;
-  static constexpr int SPB2 = SPB > NTO ? NTO : SPB, NSTRIP = NB * SPB2;
-  __device__ static int blk(int st) { return st / SPB2; }
-};
-
-template <int CIN_PAD, int COUT_PAD, int TT, int FM, int FN>
-__device__ __forceinline__ void epi_act(const AcArgs& p, const f32x16_t (&acc)[FM][FN], int b, int len, int t_out,
-                                        const float (&bias_r)[FN], float la0, float lb0) {
-  constexpr int NB = COUT_PAD / 32, PX = NB * 64, TO = TT - 32;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* win = smem;                                   // [TT][PX] (the conv's LDS is consumed)
-  const float* tl = reinterpret_cast<const float*>(smem + epi_tl_off<CIN_PAD, COUT_PAD, TT>());  // 12 up, 12 down
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
-  const int Cout = p.Cout;
-  const int c0 = t_out - 7;  // time of window row 0
-  // conv rows -> window (bf16 of acc + bias: exactly what the conv-only epilogue stores with alpha 1)
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int n = 0; n < FN; ++n) {
-      const int col = 32 * n + r32;
-      const float bc = bias_r[n];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * (wave + 4 * i) + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float v = col < Cout ? acc[i][n][r] + bc : 0.f;
-        *reinterpret_cast<uint16_t*>(win + itts_actm::woff<PX>(row, col)) = f2bf(v);
-      }
-    }
-  __syncthreads();
-  // rows outside [1, TO + 12] -> 0; rows at times outside [0, len) -> the row of the clamped time
-  // (16-B vectors along the channels; a row's swizzle permutes its own 16-B slots, so slot-wise copies are
-  // row copies)
-  constexpr int CV = NB * 4;
-  for (int v = tid; v < TT * CV; v += 256) {
-    const int r = v / CV, cs = v - r * CV;
-    const int t = c0 + r;
-    if (r >= 1 && r <= TO + 12 && t >= 0 && t < len) continue;
-    u32x4_t val{0u, 0u, 0u, 0u};
-    if (r >= 1 && r <= TO + 12) {
-      const int rs = min(max(t, 0), len - 1) - c0;
-      val = *reinterpret_cast<const u32x4_t*>(win + itts_actm::woff<PX>(rs, cs * 8));
-    }
-    *reinterpret_cast<u32x4_t*>(win + itts_actm::woff<PX>(r, cs * 8) + 0) = val;
-  }
-  __syncthreads();
-  // strips: each 32-channel block's TO / 32 output tiles cut into contiguous strips (one per wave, for
-  // NB <= 2 four / two strips per block), a strip carrying its up tile from one output tile to the next
-  using ES = EpiStrips<COUT_PAD, TT>;
-  constexpr int NTO = ES::NTO, SPB2 = ES::SPB2, NSTRIP = ES::NSTRIP;
-  itts_actm::Taps T;
-  itts_actm::make_taps(tl, T);
-  uint16_t* y = p.y + (int64_t)b * p.syb;
-  for (int st = wave; st < NSTRIP; st += 4) {
-    const int blk = ES::blk(st), k = st - blk * SPB2;
-    const int tile0 = (k * NTO) / SPB2, tile1 = ((k + 1) * NTO) / SPB2;
-    const int cb = 32 * blk;
-    const int ch = cb + r32;
-    float la = la0, lb = lb0;  // loaded at the kernel start for the wave's first strip
-    if (st != wave) {
-      la = ch < Cout ? p.plog_alpha[ch] : 0.f;
-      lb = ch < Cout ? p.plog_beta[ch] : 0.f;
-    }
-    const float a_rev = ch < Cout ? expf(la) * 0.15915494309189535f : 0.f;
-    const float inv_b = ch < Cout ? 1.0f / (expf(lb) + 1e-9f) : 0.f;
-    const int ts = t_out + 32 * tile0;
-    const int ntile = min(tile1 - tile0, max(0, (len - ts + 31) / 32));
-    itts_actm::strip<PX>(win, 32 * tile0, cb, ntile, T, a_rev, inv_b, [&](int i, const f32x16_t& a) {
-      const int t = ts + 32 * i + r32;
-      if (t < 3 || t >= len - 3) return;  // edges: exact formula below
-      uint16_t* yr = y + (int64_t)t * p.ldy + cb + 4 * h;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (cb + 8 * g + 4 * h < Cout) {
-          const u32x2_t o{pack2bf(a[4 * g], a[4 * g + 1]), pack2bf(a[4 * g + 2], a[4 * g + 3])};
-          *reinterpret_cast<u32x2_t*>(yr + 8 * g) = o;
-        }
-      }
-    });
-  }
-  // outputs within 3 samples of an utterance edge (the down-sampler's replicate pad): VALU formula
-  if (t_out < 3 || t_out + TO > len - 3) {
-    const int te = min(t_out + TO, len);
-    for (int it = tid; it < 6 * COUT_PAD; it += 256) {
-      const int e = it / COUT_PAD, cc = it - e * COUT_PAD;
-      const int t = e < 3 ? e : len - 6 + e;
-      if (t < t_out || t >= te || t < 0 || (e >= 3 && t < 3) || cc >= Cout) continue;
-      const float a = expf(p.plog_alpha[cc]) * 0.15915494309189535f;
-      const float ib = 1.0f / (expf(p.plog_beta[cc]) + 1e-9f);
-      y[(int64_t)t * p.ldy + cc] = f2bf(itts_actm::exact_at<PX>(win, c0, t, len, cc, tl, a, ib));
-    }
-  }
-}
-
-// EPI (round 5): the NEXT Activation1d applied to the conv output in the epilogue (conv1 -> act2 of an
-// AMPBlock1 layer, models.py:65-74): the tile computes conv rows t0 - 7 .. t0 + TT - 8 into an LDS window and
-// runs the MFMA activation (act_mfma.h) over it for outputs t0 .. t0 + TT - 33 -- the window and its
-// replicate-clamped rows exactly as the activation kernel (act.hip) builds them from the conv's stored
-// output, so the result is bit-identical to conv -> bf16 -> activation, without the conv output's HBM
-// write and re-read.  No residuals, alpha 1.
-template <int CIN_PAD, int COUT_PAD, int TT, bool ACT, int CK, bool EPI = false>
+template <int CIN_PAD, int COUT_PAD, int TT, bool ACT, int CK>
 __device__ __forceinline__ void amp_conv_body(const AcArgs& p) {
-  static_assert(!(EPI && ACT), "a pre-activation and an epilogue activation are not combined");
   constexpr int WS = (CIN_PAD + 31) / 32 * 32;
   constexpr int PA = CIN_PAD * 2 + 16;  // activated-window row pitch (bytes)
   constexpr int FN = COUT_PAD / 32, KS = CIN_PAD / 16, FM = TT / 128;
   constexpr int SR = 16;                // activation rows per work item
-  constexpr int TO = EPI ? TT - 32 : TT;  // output rows per tile
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.z;
   const int len = p.lens ? p.lens[b] : p.Tmax;
-  const int t_out = blockIdx.x * TO;        // first output row of the tile
-  if (t_out >= len) return;
-  const int q0 = EPI ? t_out - 7 : t_out;   // conv row 0 of the tile
+  const int q0 = blockIdx.x * TT;  // first output (= conv) row of the tile
+  if (q0 >= len) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Cin = CK ? CK : p.Cin, Cout = CK ? CK : p.Cout;
   const int WR = TT + p.hl + p.hr;  // activated window rows: t = q0 - hl + r
   constexpr bool act = ACT;  // compile-time: the no-activation variant keeps its registers for the conv
   const uint16_t* X = p.x + (int64_t)b * p.sxb;
-  // EPI: the epilogue's constants (bias, act2's taps and this wave's alpha / beta) requested now, beside the
-  // window loads, instead of three dependent global round trips in the epilogue
-  float epi_bias[EPI ? FN : 1], epi_la = 0.f, epi_lb = 0.f, epi_tap = 0.f;
-  if constexpr (EPI) {
-#pragma unroll
-    for (int n = 0; n < FN; ++n) {
-      const int col = 32 * n + (lane & 31);
-      epi_bias[n] = col < Cout ? p.bias[col] : 0.f;
-    }
-    const int ch = 32 * EpiStrips<COUT_PAD, TT>::blk(wave) + (lane & 31);
-    if (wave < EpiStrips<COUT_PAD, TT>::NSTRIP && ch < Cout) {
-      epi_la = p.plog_alpha[ch];
-      epi_lb = p.plog_beta[ch];
-    }
-    if (tid < 24) epi_tap = tid < 12 ? p.pup[tid] : p.pdown[tid - 12];
-  }
   unsigned char* Aw = smem;                         // [WR][PA]
   unsigned char* Xr = smem + (TT + kSpan) * PA;     // raw window, then the tap-weight ring
 
@@ -279,9 +144,6 @@ __device__ __forceinline__ void amp_conv_body(const AcArgs& p) {
         *reinterpret_cast<u32x4_t*>(Aw + r * PA + c * 2) = lv[i];
       }
     }
-  }
-  if constexpr (EPI) {
-    if (tid < 24) reinterpret_cast<float*>(smem + epi_tl_off<CIN_PAD, COUT_PAD, TT>())[tid] = epi_tap;
   }
   __syncthreads();
 
@@ -359,14 +221,14 @@ __device__ __forceinline__ void amp_conv_body(const AcArgs& p) {
   const uint16_t* R2 = p.r2 ? p.r2 + (int64_t)b * p.syb + (int64_t)q0 * p.ldy : nullptr;
   u32x4_t rv1[kEV], rv2[kEV];
   // clamped unconditional loads (see the window loads); lanes past nvec do not store
-  if (R1 && !EPI) {
+  if (R1) {
 #pragma unroll
     for (int i = 0; i < kEV; ++i) {
       const int e = min(tid + 256 * i, nvec - 1) * 8, r = e / Cout, c = e - r * Cout;
       rv1[i] = ld_stream(reinterpret_cast<const u32x4_t*>(R1 + (int64_t)r * p.ldy + c));
     }
   }
-  if (R2 && !EPI) {
+  if (R2) {
 #pragma unroll
     for (int i = 0; i < kEV; ++i) {
       const int e = min(tid + 256 * i, nvec - 1) * 8, r = e / Cout, c = e - r * Cout;
@@ -435,9 +297,6 @@ __device__ __forceinline__ void amp_conv_body(const AcArgs& p) {
     __syncthreads();
   }
 
-  if constexpr (EPI) {
-    epi_act<CIN_PAD, COUT_PAD, TT, FM, FN>(p, acc, b, len, t_out, epi_bias, epi_la, epi_lb);
-  } else {
   // ---- 4. epilogue: acc -> LDS f32 tile [TT][Cout] (overlays the window + ring) -> bias /
   //         residuals / alpha -> 16-B stores ----
   float* Ys = reinterpret_cast<float*>(smem);
@@ -480,12 +339,11 @@ __device__ __forceinline__ void amp_conv_body(const AcArgs& p) {
     for (int k = 0; k < 4; ++k) out[k] = pack2bf(p.alpha * o[2 * k], p.alpha * o[2 * k + 1]);
     *reinterpret_cast<u32x4_t*>(Y + off) = out;
   }
-  }  // !EPI
 }
 
-template <int CIN_PAD, int COUT_PAD, int TT, bool ACT, int CK, bool EPI = false>
+template <int CIN_PAD, int COUT_PAD, int TT, bool ACT, int CK>
 __global__ __launch_bounds__(256) void amp_conv_kernel(AcArgs p) {
-  amp_conv_body<CIN_PAD, COUT_PAD, TT, ACT, CK, EPI>(p);
+  amp_conv_body<CIN_PAD, COUT_PAD, TT, ACT, CK>(p);
 }
 
 // the same with the register budget of 3 waves per SIMD, for instantiations whose LDS allows 3
@@ -524,20 +382,6 @@ void launch_ac(const AcArgs& a, hipStream_t s) {
     if (ck) launch_one<CIK, CO, TTC, false, CKN>(a, s);
     else launch_one<CI, CO, TTC, false, 0>(a, s);
   }
-}
-
-// conv + the activation of its output (EPI): tiles of TT - 32 output rows
-template <int CI, int CO, int TT, int CK>
-void launch_epi(const AcArgs& a, hipStream_t s) {
-  constexpr int PA = CI * 2 + 16;
-  const size_t ring = (size_t)2 * CO * (CI * 2 + 16);
-  const size_t win = (size_t)(TT + kSpan) * PA;
-  const size_t lds = (size_t)epi_tl_off<CI, CO, TT>() + 128;  // conv / activation window, then the taps
-  (void)win;
-  (void)ring;
-  constexpr int TO = TT - 32;
-  dim3 grid((a.Tmax + TO - 1) / TO, 1, a.B);
-  hipLaunchKernelGGL((amp_conv_kernel<CI, CO, TT, false, CK, true>), grid, dim3(256), lds, s, a);
 }
 
 }  // namespace
@@ -595,56 +439,5 @@ extern "C" int itts_amp_conv_fwd(const void* x, int64_t x_sb, int64_t ldx, const
   else if (ci == 64 && co == 64) launch_ac<64, 64, ITTS_AMP_TT64, ITTS_AMP_TTC64, 48, ITTS_AMP_K48>(a, s);
   else if (ci == 96 && co == 96) launch_ac<96, 96, ITTS_AMP_TT96, ITTS_AMP_TTC96, 96, 96>(a, s);
   else return itts::fail(fn, "supported (Cin, Cout) padded pairs: (32,32), (64,64), (96,96)");
-  return itts::check_launch(fn);
-}
-
-extern "C" int itts_amp_conv_act_fwd(const void* x, int64_t x_sb, int64_t ldx, const void* w_packed, const float* bias,
-                                     void* y, int64_t y_sb, int64_t ldy, const int32_t* lengths, int B, int Tmax,
-                                     int Cin, int Cout, int ntaps, const int32_t* tap_off, const float* up12,
-                                     const float* down12, const float* log_alpha, const float* log_beta,
-                                     void* stream) {
-  const char* fn = "itts_amp_conv_act_fwd";
-  ITTS_REQUIRE(B >= 0 && Tmax >= 0 && Cin > 0 && Cout > 0, fn, "bad sizes");
-  if (B == 0 || Tmax == 0) return 0;
-  ITTS_REQUIRE(x && w_packed && bias && y && tap_off && lengths, fn, "null pointer");
-  ITTS_REQUIRE(up12 && down12 && log_alpha && log_beta, fn, "the activation needs filters and alpha / beta");
-  ITTS_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && x_sb % 8 == 0 && y_sb % 8 == 0,
-               fn, "channels / strides must be multiples of 8 (16-B vectors)");
-  ITTS_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0, fn,
-               "tensors must be 16-B aligned");
-  ITTS_REQUIRE(ntaps >= 1 && ntaps <= kMaxTapsAc, fn, "ntaps must be in [1, 16]");
-  AcArgs a{};
-  a.x = static_cast<const uint16_t*>(x);
-  a.sxb = x_sb;
-  a.ldx = ldx;
-  a.pup = up12;
-  a.pdown = down12;
-  a.plog_alpha = log_alpha;
-  a.plog_beta = log_beta;
-  a.w = static_cast<const uint16_t*>(w_packed);
-  a.bias = bias;
-  a.y = static_cast<uint16_t*>(y);
-  a.syb = y_sb;
-  a.ldy = ldy;
-  a.lens = lengths;
-  a.B = B;
-  a.Tmax = Tmax;
-  a.Cin = Cin;
-  a.Cout = Cout;
-  a.ntaps = ntaps;
-  a.alpha = 1.0f;
-  int lo = 0, hi = 0;
-  for (int j = 0; j < ntaps; ++j) {
-    a.tap_off[j] = tap_off[j];
-    lo = tap_off[j] < lo ? tap_off[j] : lo;
-    hi = tap_off[j] > hi ? tap_off[j] : hi;
-  }
-  a.hl = -lo;
-  a.hr = hi;
-  ITTS_REQUIRE(hi - lo <= kSpan, fn, "tap span exceeds 64 rows");
-  hipStream_t s = itts::as_stream(stream);
-  if (Cin == 24 && Cout == 24) launch_epi<32, 32, ITTS_AMP_TT32, 24>(a, s);
-  else if (Cin == 48 && Cout == 48) launch_epi<ITTS_AMP_K48, 64, ITTS_AMP_TT64, 48>(a, s);
-  else return itts::fail(fn, "supported channel counts: 24, 48 (the BigVGAN narrow stages)");
   return itts::check_launch(fn);
 }

@@ -10,6 +10,8 @@
 // applies 1/n_blocks.  Tail: activation_post -> conv_post + tanh (+ int16).  Channel-last bf16
 // activations [B][T_stage][C] in six workspace buffers; per-stage lengths and the speaker biases at
 // the workspace start.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -37,6 +39,15 @@ int64_t align256(int64_t v) { return (v + 255) / 256 * 256; }
 // whose cout = up_rate * C holds the phases as output column blocks (row q of the [T][u*C] output is
 // rows q*u .. q*u+u-1 of the [T*u][C] stage input): fused when phases[0].cout == u * C, C the AMP
 // layers' channel count.
+// ITTS_VOC_TAIL_FUSED=0: activation_post and conv_post as two launches (the fused launch is bit-identical)
+bool tail_fused() {
+  static const bool on = [] {
+    const char* e = getenv("ITTS_VOC_TAIL_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool fused_up(const ItTsBigvganStage& st) {
   return st.up_rate > 1 && st.n_blocks > 0 && st.n_layers > 0 && st.layers &&
          st.phases[0].cout == st.up_rate * st.layers[0].c1.cout;
@@ -127,10 +138,6 @@ extern "C" int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* lat
                              a ? a->log_alpha : nullptr, a ? a->log_beta : nullptr, c.w, c.bias, r1, r2, y,
                              (int64_t)Tx * c.cout, c.cout, ln, B, Tx, c.cin, c.cout, c.ntaps, c.tap_off, alpha, stream);
   };
-  auto amp_act = [&](const ItTsConv& c, const uint16_t* x, int Tx, uint16_t* y, const int32_t* ln, const ItTsAct& a) {
-    return itts_amp_conv_act_fwd(x, (int64_t)Tx * c.cin, c.cin, c.w, c.bias, y, (int64_t)Tx * c.cout, c.cout, ln, B, Tx,
-                                 c.cin, c.cout, c.ntaps, c.tap_off, a.up12, a.down12, a.log_alpha, a.log_beta, stream);
-  };
   auto act = [&](const ItTsAct& a, const uint16_t* x, uint16_t* y, int C, int Tx, const int32_t* ln) {
     return itts_aa_snakebeta_fwd(x, y, a.up12, a.down12, a.log_alpha, a.log_beta, ln, B, C, Tx, (int64_t)Tx * C, C, 1,
                                  (int64_t)Tx * C, C, 1, ITTS_BF16, ITTS_BF16, stream);
@@ -162,10 +169,6 @@ extern "C" int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* lat
         if (st.amp_mode == 1) {  // activation fused into the conv's input staging
           rc = amp(ly.c1, src, Tn, t2, ln, &ly.a1, nullptr, nullptr, 1.0f);
           if (!rc) rc = amp(ly.c2, t2, Tn, dst, ln, &ly.a2, src, r2, alpha);
-        } else if (st.amp_mode == 3) {  // act kernel, conv1 with act2 in its epilogue, conv2 (+ residuals)
-          rc = act(ly.a1, src, t1, C, Tn, ln);
-          if (!rc) rc = amp_act(ly.c1, t1, Tn, t2, ln, ly.a2);
-          if (!rc) rc = amp(ly.c2, t2, Tn, dst, ln, nullptr, src, r2, alpha);
         } else if (st.amp_mode == 2) {  // activation kernel + the conv kernel without activation
           rc = act(ly.a1, src, t1, C, Tn, ln);
           if (!rc) rc = amp(ly.c1, t1, Tn, t2, ln, nullptr, nullptr, nullptr, 1.0f);
@@ -186,6 +189,12 @@ extern "C" int itts_bigvgan_forward(const ItTsBigvganWeights* w, const void* lat
   if (rc) return rc;
   const int Cl = stage_channels(w->stages[ns - 1]);
   const int32_t* ln = lens + (int64_t)ns * B;
+  // activation_post + conv_post + tanh (+ int16): one launch where the last stage is one MFMA channel block
+  // (IndexTTS-1.5: 24 channels; bit-identical to the two launches below)
+  if (Cl % 8 == 0 && Cl <= 32 && (w->post_k & 1) && w->post_k <= 15 && tail_fused())
+    return itts_act_conv_post_tanh(cur_in, (int64_t)Tcur * Cl, Cl, w->act_post.up12, w->act_post.down12,
+                                   w->act_post.log_alpha, w->act_post.log_beta, w->post_w, w->post_b, Cl, w->post_k, ln,
+                                   B, Tcur, wav, pcm, Tcur, stream);
   rc = act(w->act_post, cur_in, t1, Cl, Tcur, ln);
   if (rc) return rc;
   return itts_conv_post_tanh(t1, (int64_t)Tcur * Cl, Cl, w->post_w, w->post_b, Cl, w->post_k, ln, B, Tcur, wav, pcm,

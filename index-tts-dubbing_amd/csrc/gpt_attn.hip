@@ -80,6 +80,12 @@ constexpr int kSub = 4;  // keys per group per online-softmax update (every KB i
 #ifndef ITTS_KV_NT
 #define ITTS_KV_NT 1
 #endif
+// beams (ROWS): the beams of an utterance read the same lineage rows at about the same time (neighbouring
+// workgroups of one XCD), so their K/V loads keep the default cache policy -- a non-temporal line is not kept in
+// L2 for the next beam's read (round 6, profiles/r06_b3nt.txt); ITTS_BEAM_KV_NT=1: non-temporal as greedy (A/B)
+#ifndef ITTS_BEAM_KV_NT
+#define ITTS_BEAM_KV_NT 0
+#endif
 constexpr int kAttnKviMax = 3584;  // beams: keys per row whose lineage indices the kernel stages in LDS
 template <typename TC, typename TO, int NT, bool ROWS, bool PROJ, int KB = ITTS_ATTN_KB>
 __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void attn_decode_kernel(const float* __restrict__ qkv, int64_t ldqkv, int nsplit,
@@ -149,11 +155,10 @@ __global__ __launch_bounds__(NT, PROJ ? ITTS_ATTN_PROJ_WPS : ITTS_ATTN_WPS) void
 #pragma unroll
       for (int w = 0; w < RW; ++w) {
         const u32x4_t* src = reinterpret_cast<const u32x4_t*>(base + koff(p0 + j) + 8 * d8) + w;
-#if ITTS_KV_NT
-        dst[u][w] = __builtin_nontemporal_load(src);
-#else
-        dst[u][w] = *src;
-#endif
+        if constexpr (ITTS_KV_NT && (!ROWS || ITTS_BEAM_KV_NT))
+          dst[u][w] = __builtin_nontemporal_load(src);
+        else
+          dst[u][w] = *src;
       }
     }
   };

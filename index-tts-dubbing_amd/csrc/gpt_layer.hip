@@ -71,12 +71,6 @@ constexpr int kKB = ITTS_PL_KB;  // attention keys per group per round (load dep
 #define ITTS_PL_SMALL_ROWS 16
 #endif
 constexpr int kKBSmall = ITTS_PL_KB_SMALL, kSmallRows = ITTS_PL_SMALL_ROWS;
-#ifndef ITTS_PL_KEEP_QKV  // every layer's c_attn operands with the default cache policy (A/B)
-#define ITTS_PL_KEEP_QKV 1
-#endif
-#ifndef ITTS_PL_DMA_LATE
-#define ITTS_PL_DMA_LATE 0
-#endif
 #ifndef ITTS_PL_KV_UNCOND
 #define ITTS_PL_KV_UNCOND 1
 #endif
@@ -87,6 +81,9 @@ constexpr int kKBSmall = ITTS_PL_KB_SMALL, kSmallRows = ITTS_PL_SMALL_ROWS;
 #define ITTS_PL_SMALL_H16 1
 #endif
 constexpr bool kSmallH16 = ITTS_PL_SMALL_H16 != 0;
+#ifndef ITTS_BEAM_KV_NT
+#define ITTS_BEAM_KV_NT 0
+#endif
 static_assert(kSmallRows <= 16, "small steps fit one 16-row half");
 static_assert(kKB % 4 == 0 && kKBSmall % 4 == 0, "keys per round: whole kSub chunks");
 constexpr int kSub = 4;                               // keys per online-softmax chunk (gpt_attn.hip)
@@ -99,51 +96,14 @@ constexpr uint32_t kSpinMax = 1u << 19;               // bounded spins (~0.3 s),
 #ifndef ITTS_PL_TRACE_LAYER
 #define ITTS_PL_TRACE_LAYER 10
 #endif
-// ITTS_PL_DMA_EARLY=1: the later phases' weight DMA is issued at launch start, ahead of the c_attn
-// operands' arrival (round-4 first version); default: right after the c_attn MFMAs, so the burst does
-// not queue in front of the critical-path loads (profiles/pl_trace_r04*.txt)
-#ifndef ITTS_PL_DBG
-#define ITTS_PL_DBG 0
-#endif
-// A/B switches for the hand-off memory protocol: ITTS_PL_SYS=1 makes every hand-off access system scope
-// (sc0 sc1), ITTS_PL_ACQ=1 adds an agent-scope acquire after every matched poll / granule sweep
-#ifndef ITTS_PL_SYS
-#define ITTS_PL_SYS 0
-#endif
-#ifndef ITTS_PL_ACQ
-#define ITTS_PL_ACQ 0
-#endif
-#if ITTS_PL_SYS
-#define PL_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
-#define PL_AUX 17
-#else
+// hand-off accesses: agent scope (the grid is one device); write-through stores / loads carry sc1 (aux 16)
 #define PL_SCOPE __HIP_MEMORY_SCOPE_AGENT
-#define PL_AUX 16
-#endif
-// ITTS_PL_KV_LATE=1: pass 0's K/V rows are requested after the c_attn MFMAs (A/B: they queue in front of
-// nothing the critical path needs, but start later)
-#ifndef ITTS_PL_PART16
-#define ITTS_PL_PART16 0  // 16-B partial stores measured neutral: 663.0 vs 661.2 us per C3 step
-#endif
-#ifndef ITTS_PL_KV_LATE
-#define ITTS_PL_KV_LATE 0
-#endif
-// A/B switches measured neutral or slower (profiles/r05_xc16.sh, r05xa_ab.txt), off by default:
-//   ITTS_PL_XC16=1: phase D's x1^ copies as 16-B write-through stores (4 lanes gathered by shuffles): C3 643.3 /
-//     641.8 vs 640.6 / 642.4 us per step, C2 500.7 / 501.1 vs 499.8 / 499.3
-//   ITTS_PL_BEAM_MAJOR=1: beam lineage rows, one attention unit takes an utterance's MT beams in consecutive
-//     passes (phase A's row tiles gathered to match): beam3 1422 / 1426 vs 1334 / 1330 us -- in the default order
-//     an utterance's beams are three units of one cluster reading the same lineage rows at once (one XCD's L2);
-//     a pass apart (~8 MB of K/V per cluster) they miss the 4 MB L2
-#ifndef ITTS_PL_XC16
-#define ITTS_PL_XC16 0
-#endif
-#ifndef ITTS_PL_BEAM_MAJOR
-#define ITTS_PL_BEAM_MAJOR 0
-#endif
-#ifndef ITTS_PL_DMA_EARLY
-#define ITTS_PL_DMA_EARLY 0
-#endif
+constexpr int PL_AUX = 16;
+// Variants built, measured slower or neutral and removed in round 6 (their numbers stay in DESIGN.md §4c):
+// several layers per launch (C3 714 vs 647 us), split softmax groups for one-row steps (C2 604 vs 500 us),
+// beam-major attention rows (beam3 1422 vs 1330 us), 16-B x1^ / partial stores (neutral), pass-0 K/V after
+// c_attn (687 vs 665 us), the weight DMA at launch start (685 vs 665 us) or after the first key round (653 vs
+// 648 us), every layer's weights with the default cache policy (neutral), the debug / protocol A/B switches.
 
 // scratch layout (bytes) for up to kMaxR rows; counters, granules, the epoch and the error word are zero after
 // itts_gpt_pl_reset (and after the caller's zero fill at allocation), never between steps
@@ -155,7 +115,7 @@ constexpr int kMaxR = 128;
 #define ITTS_PL_CNT_STRIDE 1024
 #endif
 constexpr int kCntStride = ITTS_PL_CNT_STRIDE;  // u32 units
-constexpr int kNumCnt = 152;
+constexpr int kNumCnt = 88;
 constexpr int64_t kOffCnt = 0;
 constexpr int64_t kOffGq = ((int64_t)kNumCnt * kCntStride * 4 + 511) / 512 * 512;                                       // [128 rows][16 heads][192] u64
 constexpr int64_t kOffOb = kOffGq + (int64_t)kMaxR * kH * 192 * 8;    // [8][128][128] bf16
@@ -163,18 +123,12 @@ constexpr int64_t kOffP1 = kOffOb + (int64_t)kNC * kMaxR * 128 * 2;   // [8][128
 constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * kMaxR * kD * 4;    // [8][128][1024] bf16
 constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * kMaxR * kD * 2;    // [8][128][512] bf16
 constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * kMaxR * 512 * 2;   // [8][128][1024] f32
-constexpr int kPaStride = 72;                                         // floats per (head, group) partial
-constexpr int64_t kOffPa = kOffP2 + (int64_t)kNC * kMaxR * kD * 4;    // [16 heads][32 groups][72] f32 (SG)
-constexpr int64_t kOffTrace = kOffPa + (int64_t)kH * 32 * kPaStride * 4; // [256 WG][32] u64 (ITTS_PL_TRACE builds)
+constexpr int64_t kOffTrace = kOffP2 + (int64_t)kNC * kMaxR * kD * 4;  // [256 WG][32] u64 (ITTS_PL_TRACE builds)
 constexpr int64_t kOffSeq = kOffTrace + (int64_t)kWG * 32 * 8;        // u32 epoch: launches since the reset
-constexpr int64_t kOffErr = kOffSeq + 256;                             // sticky error word
-constexpr int64_t kScratchBytes = kOffErr + 256;
+constexpr int64_t kOffErr = kOffSeq + 4;  // sticky error word, beside the epoch: one 8-B load reads both
+constexpr int64_t kScratchBytes = kOffSeq + 256;
 constexpr int64_t kZeroBytes = kOffGq + (int64_t)kMaxR * kH * 192 * 8;  // counters + every granule (x16)
-// CNT7: the layer seam inside a multi-layer launch (x^ of layer l -> c_attn of layer l + 1): 8 x 8 counters
-// [producer cluster][consumer cluster], each with the 32 adders of its producer cluster and the 32 pollers of its
-// consumer cluster (workgroup 8j + c adds to CNT7 + 8c + r for every r: one wave instruction, 8 lanes; polls
-// CNT7 + 8q + c for every q, 8 lanes).  One counter for all 256 adders serialised their atomics: ~1.3 us per seam.
-enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56, CNT7 = 88 };
+enum { CNT2 = 0, CNT3 = 8, CNT4 = 40, CNT5 = 48, CNT6 = 56 };
 
 // LDS layout (bytes)
 constexpr int L_WO = 0, L_WFC = L_WO + 8 * 1024, L_WPJ = L_WFC + 32 * 1024, L_RED = L_WPJ + 32 * 1024;
@@ -191,7 +145,7 @@ constexpr int kRestBytes = kLdsBytes - L_RED;  // everything after the weight sl
 // scratch and put `s_waitcnt vmcnt(0)` (the whole 72 KiB DMA) in front of every LDS access after the
 // DMA issue; distinct objects get distinct alias scopes, so only the reads of the weights wait.
 
-// one layer's weights (kernel arguments: the launch's layers are indexed by the loop counter)
+// one layer's weights
 struct PlLayerPtrs {
   const u32x4_t* qkv_w12;  // [256][32 ks][4 q][12 c] x 16 B
   const float* qkv_uc;     // [256][2][12]
@@ -202,30 +156,24 @@ struct PlLayerPtrs {
   const u32x4_t* proj_w;   // mlp.c_proj, pack_skinny [32 tiles][256 ks][64][8]
   const float* proj_b;
 };
-constexpr int kMaxLpl = 32;  // layers per launch (kernel-argument table; 32 x 72 B)
 // beams (kv_rows): each attention unit stages its row's lineage indices (keys 0 .. nk-1) in LDS, so a key
 // round's K/V addresses need an LDS read, not a global load whose vmcnt wait (in order) also waited for the
 // round's V rows still in flight; max_kv of a beam state must not exceed this
 constexpr int kKviMax = 3584;
-struct PlCommon {
+struct PlArgs {
   float* x;                // [R][1024] f32
   uint16_t* xh;            // [32][1024] bf16 (rows >= R: read, never written)
-  uint16_t *kc, *vc;       // layer `layer`'s cache [R][16][max_kv][64]; layer + i at + i * layer_cache
-  int64_t cache_bs, cache_hs, layer_cache;
+  uint16_t *kc, *vc;       // this layer's cache [R][16][max_kv][64]
+  int64_t cache_bs, cache_hs;
   const int32_t* pad;
   const int32_t* tstate;
   const int32_t* kv_rows;  // beams: [R][ld_rows] cache row of each prefix position, else null
   int64_t ld_rows;
-  int kv_base, kstep, R, layer, nl, last;  // layers layer .. layer + nl - 1; last: the model's last among them
-  int seam;  // every layer adds to the CNT7 seam counters (a process that runs multi-layer launches)
+  int kv_base, kstep, R, layer, last;  // last: the model's last layer (its x2 reduce runs outside, with ln_f)
   float eps;
   unsigned char* scratch;
+  PlLayerPtrs ly;
 };
-template <int NLY>
-struct PlArgsT : PlCommon {
-  PlLayerPtrs ly[NLY];
-};
-// one-layer launches keep the round-4 argument size (~200 B); multi-layer launches carry the whole table
 
 // workgroup barrier that waits for this wave's LDS traffic only: a __syncthreads() would also drain
 // every vector-memory load in flight (the K/V rows requested ahead of the c_attn phase)
@@ -234,7 +182,14 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
-constexpr int kDropLimit = 0x7fff0000, kDrop = 0x7ffffff0;  // cancelled buffer stores (see rsrc_of_lim)
+// Cancelled buffer stores (row tiles > 1): a lane with nothing to store hands its buffer store the offset kDrop,
+// past the range kDropLimit of every descriptor such a store uses, and the hardware drops it.  kDrop must lie past
+// the range under either bounds rule (offset >= range, or offset + size > range), and ONLY buffer stores whose
+// descriptor carries the kDropLimit range may ever see it: with the full 0x7fffffff range a 2- or 8-byte store at
+// 0x7ffffff0 is in range and lands 2 GiB past the base (the r05t illegal address).  The host checks
+// that every real offset such a descriptor addresses lies below kDropLimit (check_state: the K/V cache extent).
+constexpr int kDropLimit = 0x7fff0000, kDrop = 0x7ffffff0;
+static_assert(kDrop >= kDropLimit && (int64_t)kDrop + 2 > kDropLimit, "cancelled stores must be out of range");
 // s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= n only (expcnt / lgkmcnt at their maxima)
 constexpr int vm_wait_enc(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 // every storing wave's write-through stores have left (Guideline 16 R1: before the counter add)
@@ -257,13 +212,7 @@ __device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
 // signed difference); returns false on timeout / a failed grid
 __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uint32_t code) {
   for (uint32_t n = 0;; ++n) {
-    if ((int32_t)(ld_relaxed(ctr) - target) >= 0) {
-      if (ITTS_PL_ACQ) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      return true;
-    }
+    if ((int32_t)(ld_relaxed(ctr) - target) >= 0) return true;
     if ((n & 255) == 255 && ld_relaxed(err) != 0) return false;
     if (n > kSpinMax) {
       __hip_atomic_store(err, code, __ATOMIC_RELAXED, PL_SCOPE);
@@ -273,19 +222,12 @@ __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uin
   }
 }
 
-// WKEEP: this layer's weights read with the default cache policy instead of non-temporal, so that they can
-// stay in the 256-MiB Infinity Cache from one decode step to the next (the whole step streams 520 MB of
-// weights + the K/V, all non-temporal otherwise; ITTS_PL_KEEP_LAYERS picks how many layers)
 // H16 (steps of at most 16 rows, MT = 1): the c_attn / c_fc phases load and multiply only the first 16-row
 // half of their A operands (rows 16-31 are padding: their outputs, never read, come out as the fold terms)
-// MULTI: the launch runs p.nl layers joined by the seam; else one layer (p.nl == 1), straight-line code
-// SG (one-row steps, C2): the 32 softmax groups of each head spread over the cluster's 64 attention units (one
-// group each, every lane group of the unit computing the same one) instead of one unit per head; the groups'
-// (m, l, o) partials are merged in phase C in the in-unit merge's exact order (bit-identical)
-template <int MT, bool ROWS, int KB = kKB, bool WKEEP = false, bool H16 = false, bool MULTI = false, bool SG = false>
-__global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? kMaxLpl : 1> p) {
+template <int MT, bool ROWS, int KB = kKB, bool H16 = false>
+__global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   static_assert(!H16 || MT == 1, "16-row halves: one row tile");
-  constexpr int WAUX = WKEEP ? 0 : 2;  // LDS-DMA cache policy of the weight stream
+  constexpr int WAUX = 2;              // LDS-DMA cache policy of the weight stream: non-temporal
   constexpr int NHF = H16 ? 1 : 2;     // 16-row halves of the A operands loaded / multiplied
   __shared__ __attribute__((aligned(16))) unsigned char lds_wo[8 * 1024];
   __shared__ __attribute__((aligned(16))) unsigned char lds_wfc[32 * 1024];
@@ -294,38 +236,26 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   __shared__ int32_t lds_kvi[ROWS ? 2 * kKviMax : 1];  // [unit][key] lineage cache rows (beams)
   unsigned char* const smem = lds_rest - L_RED;  // offsets >= L_RED address lds_rest
   typedef __attribute__((address_space(3))) void lds_void;
+  const PlLayerPtrs& Ly = p.ly;
   const int b = blockIdx.x;
-  int c = b % kNC, j = b / kNC;  // (MULTI: laundered per layer)
-  int zz = 0;  // MULTI: an opaque zero per layer (see the layer loop)
-  int tid = threadIdx.x, lane = tid & 63;  // (laundered per layer: see the layer loop)
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int hh = j >> 4, jj = j & 15, h = 2 * c + hh;
-  // scratch regions.  MULTI: every use takes a fresh opaque copy of the scratch base, so the compiler cannot keep
-  // the dozen derived pointers / buffer descriptors live across the whole layer loop (they spilled: 118 SGPRs to
-  // VGPR lanes, a readlane in every phase)
-  auto scr = [&]() __attribute__((always_inline)) {
-    unsigned char* q = p.scratch;
-    if constexpr (MULTI) asm volatile("" : "+s"(q));
-    return q;
-  };
-  auto cnt_ = [&](int i) __attribute__((always_inline)) {
-    return reinterpret_cast<uint32_t*>(scr() + kOffCnt) + (int64_t)i * kCntStride;
-  };
-  auto err_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<uint32_t*>(scr() + kOffErr); };
-  uint32_t* seq = reinterpret_cast<uint32_t*>(p.scratch + kOffSeq);
-  // (no err check here: it cost a memory round trip before the first load; every poll and granule sweep
-  // checks err every 256 spins, so after a timeout the grid still drains within one spin round per phase)
-  auto gq_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<uint64_t*>(scr() + kOffGq); };
-  auto p1_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<float*>(scr() + kOffP1); };
-  auto p2_ = [&]() __attribute__((always_inline)) { return reinterpret_cast<float*>(scr() + kOffP2); };
+  const int c = b % kNC, j = b / kNC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = j >> 4, jj = j & 15, h = 2 * c + hh;
+  uint32_t* const cnt = reinterpret_cast<uint32_t*>(p.scratch + kOffCnt);
+  auto cnt_ = [&](int i) { return cnt + (int64_t)i * kCntStride; };
+  uint32_t* const err = reinterpret_cast<uint32_t*>(p.scratch + kOffErr);
+  uint32_t* const seq = reinterpret_cast<uint32_t*>(p.scratch + kOffSeq);
+  uint64_t* const gq = reinterpret_cast<uint64_t*>(p.scratch + kOffGq);
+  float* const p1 = reinterpret_cast<float*>(p.scratch + kOffP1);
+  float* const p2 = reinterpret_cast<float*>(p.scratch + kOffP2);
+  unsigned char* const xc = p.scratch + kOffXc;
   auto rsrc_of = [&](int64_t off) __attribute__((always_inline)) {
-    return __builtin_amdgcn_make_buffer_rsrc(scr() + off, 0, 0x7fffffff, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(p.scratch + off, 0, 0x7fffffff, 0x00020000);
   };
-  auto xc = [&]() __attribute__((always_inline)) { return scr() + kOffXc; };
   // descriptors whose stores a lane can cancel: range kDropLimit, and a cancelled lane's offset kDrop lies past it
-  // (offset >= range and offset + size > range: dropped under either bounds rule)
-  auto rsrc_of_lim = [&](int64_t off) __attribute__((always_inline)) {
-    return __builtin_amdgcn_make_buffer_rsrc(scr() + off, 0, kDropLimit, 0x00020000);
+  auto rsrc_lim = [&](void* base) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, kDropLimit, 0x00020000);
   };
   float* red = reinterpret_cast<float*>(smem + L_RED);
   float* rsum = reinterpret_cast<float*>(smem + L_STAT);
@@ -337,30 +267,26 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   const int R = p.R;
   if (tid == 0) *abort_flag = 0;
   uint64_t* trace = reinterpret_cast<uint64_t*>(p.scratch + kOffTrace) + 32 * b;
-  int cur_layer = p.layer;  // the model layer the loop is in (trace / debug marks)
   auto mark = [&](int i) {
-    if (ITTS_PL_TRACE && cur_layer == ITTS_PL_TRACE_LAYER && tid == 0) trace[i] = __builtin_amdgcn_s_memrealtime();
+    if (ITTS_PL_TRACE && p.layer == ITTS_PL_TRACE_LAYER && tid == 0) trace[i] = __builtin_amdgcn_s_memrealtime();
   };
   mark(0);
-  // ITTS_PL_DBG (debug builds): layer 0 of a generate's first decode step stores what wave 0 read into
-  // trace slots 20..31 (profiles/lf_dbg.py)
-  const bool dbg_on = ITTS_PL_DBG && p.tstate[0] + p.kstep == 0 && tid == 0;
-  auto dbg = [&](int i, uint32_t v) {
-    if (dbg_on && cur_layer == 0) trace[20 + i] = v;
-  };
 
-  int w = wave;
-  int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
+  const int c16 = lane & 15, q4 = lane >> 4, r32 = lane & 31, hb = lane >> 5;
   const int kidx = p.kv_base + p.tstate[0] + p.kstep;
-  // this launch's first epoch: a plain load (written by an earlier launch) beside the step counter's, so both
-  // are waited for together before the K/V addresses (an sc1 load at launch start was waited for on its own:
-  // +12 us per step, r05a).  Layer i of the launch runs at epoch L1base + i.
-  const uint32_t L1base = *seq + 1u;
+  // this launch's epoch and the sticky error word: plain loads (written by earlier launches) beside the step
+  // counter's, so all are waited for together before the K/V addresses (an sc1 load at launch start was waited
+  // for on its own: +12 us per step, r05a).  After a hand-off timeout every later launch returns here at once, so
+  // the rest of a graph replay drains in microseconds and the host's launch-chain re-run starts right away.
+  const uint64_t seq_err = *reinterpret_cast<const uint64_t*>(seq);
+  const uint32_t L1 = (uint32_t)seq_err + 1u;
+  // a hand-off of an earlier launch timed out: this launch only runs to its q/k/v sweep and returns (no poll, no
+  // spin), so the rest of a graph replay drains in microseconds.  (Not an early return at entry: the branch would
+  // serialise this load in front of the step counter's and cost a scalar round trip on every launch.)
+  const bool dead = (uint32_t)(seq_err >> 32) != 0u;
   // attention: this workgroup's rows of head h are 32 pt + 2 jj + u (pass pt, unit u = waves 4u .. 4u+3)
-  int u = w >> 2;
-  int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
-  static_assert(!SG || (MT == 1 && H16 && !MULTI && !ROWS), "split groups: one-row small steps");
-  if constexpr (SG) g = 2 * jj + u;  // this unit's softmax group (keys g + 32 n of row 0)
+  const int u = w >> 2;
+  const int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
   constexpr int NG = 32;
   u32x4_t kr[KB], vr[KB];
   // K/V rows of key index jk (0-based from the row's first valid key) of row `row`: the row's own cache
@@ -368,24 +294,22 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   auto kv_ptr = [&](const uint16_t* cache, int row, int pos, int jk) -> const uint16_t* {
     int crow = row;
     if constexpr (ROWS) crow = lds_kvi[u * kKviMax + jk];
-    return cache + (int64_t)crow * p.cache_bs + (int64_t)(h + zz) * p.cache_hs + (int64_t)pos * kHD + 8 * d8;
+    return cache + (int64_t)crow * p.cache_bs + (int64_t)h * p.cache_hs + (int64_t)pos * kHD + 8 * d8;
   };
   auto kv_load = [&](u32x4_t (&dst)[KB], const uint16_t* cache, int row, int p0, int nk, int j0) {
 #pragma unroll
     for (int uu = 0; uu < KB; ++uu) {
       const int jk = min(j0 + NG * uu + g, max(nk - 2, 0));
-      dst[uu] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk, jk)));
+      const u32x4_t* src = reinterpret_cast<const u32x4_t*>(kv_ptr(cache, row, p0 + jk, jk));
+      // beams: default cache policy, so the other beams of the utterance (units of this cluster, one XCD) find
+      // the shared lineage rows in L2 (gpt_attn.hip ITTS_BEAM_KV_NT)
+      if constexpr (ROWS && !ITTS_BEAM_KV_NT)
+        dst[uu] = *src;
+      else
+        dst[uu] = __builtin_nontemporal_load(src);
     }
   };
-  // ITTS_PL_BEAM_MAJOR=1, beams (ROWS) with whole row tiles: unit (jj, u) takes rows MT (2 jj + u) + pt, i.e. one
-  // utterance's beams in consecutive passes (slower, see the switch: the default order has them on three units of
-  // the cluster at once, sharing the lineage rows through the XCD's L2)
-  const bool beam_major = ITTS_PL_BEAM_MAJOR && ROWS && MT > 1 && R == 32 * MT;
-  auto unit_row = [&](int pt) { return SG ? 0 : beam_major ? MT * (2 * jj + u) + pt : 32 * pt + 2 * jj + u; };
-  // phase A's row tiles gather in the same order: tile t = rows MT i + t (beam t of every utterance), so attention
-  // pass pt needs only tile pt's q/k/v and the tiles keep overlapping the passes (row-independent arithmetic:
-  // every row's c_attn output is the same in any tile)
-  auto a_row = [&](int t, int i) { return beam_major ? MT * i + t : 32 * t + i; };
+  auto unit_row = [&](int pt) { return 32 * pt + 2 * jj + u; };
   // beams: this unit's lineage indices of row `row` (keys 0 .. nk-1) into LDS; every thread of the workgroup
   // calls it (it ends with the barrier the readers need)
   auto stage_kvi = [&](int row, int p0, int nk) __attribute__((always_inline)) {
@@ -395,14 +319,14 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       bar();
     }
   };
-  int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns per tile
+  const int xrow = tid >> 4, xcol = 32 * j + 2 * (tid & 15);  // phases D / G: this thread's 2 columns per tile
   // (phase G: wave w holds rows 4w .. 4w+3 of every row tile, xrow >> 2 == w)
 
-  // ---- (A0) c_attn operands first (weights nt, 12 of 16 fragment columns real; A = x^ tile 0), then the
-  // attention's first round of K/V rows (pass 0), then the residual slices, then the weight DMA
+  // ---- (A0) c_attn operands first (12 of 16 fragment columns real, default cache policy: 126 MB over the
+  // layers that can stay in the Infinity Cache; A = x^ tile 0), then the attention's first round of K/V rows
+  // (pass 0), then the residual slices; the weight DMA goes out after the q/k/v sweep
   u32x4_t bw[4], av[4][2];
-  // the residual slices (rows xrow of every tile, this thread's 2 columns): the launch's first layer loads them
-  // (issued first, selected at phase D: no early wait on them); a later layer gets them from phase G
+  // the residual slices (rows xrow of every tile, this thread's 2 columns), selected at phase D: no early wait
   float2 x_raw[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
@@ -415,76 +339,53 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   // waves issue the whole burst, so unit 0's later K/V rounds do not retire behind it (in-order vmcnt) -- at
   // one row per head those few units are the critical path
   const bool dma_split = ITTS_PL_DMA_SPLIT && H16 && 2 * jj < R && 2 * jj + 1 >= R;  // workgroup-uniform
-  auto dma_one = [&](const PlLayerPtrs& Ly, int t) {
+  auto dma_one = [&](int t) {
     // t is wave-uniform: each branch is one uniform DMA into its own LDS object
     if (t < 8)
-      __builtin_amdgcn_global_load_lds(Ly.o_w + (((int64_t)(j + zz) * 64 + 8 * c + t) * 64 + lane),
+      __builtin_amdgcn_global_load_lds(Ly.o_w + (((int64_t)j * 64 + 8 * c + t) * 64 + lane),
                                        (lds_void*)(lds_wo + t * 1024), 16, 0, WAUX);
     else if (t < 40)
-      __builtin_amdgcn_global_load_lds(Ly.fc_w16 + (((int64_t)(32 * c + j + zz) * 32 + (t - 8)) * 64 + lane),
+      __builtin_amdgcn_global_load_lds(Ly.fc_w16 + (((int64_t)(32 * c + j) * 32 + (t - 8)) * 64 + lane),
                                        (lds_void*)(lds_wfc + (t - 8) * 1024), 16, 0, WAUX);
     else
-      __builtin_amdgcn_global_load_lds(Ly.proj_w + (((int64_t)(j + zz) * 256 + 32 * c + (t - 40)) * 64 + lane),
+      __builtin_amdgcn_global_load_lds(Ly.proj_w + (((int64_t)j * 256 + 32 * c + (t - 40)) * 64 + lane),
                                        (lds_void*)(lds_wpj + (t - 40) * 1024), 16, 0, WAUX);
   };
   // straight-line issue (a data-dependent trip count leaves the compiler's vmcnt tracking a join it resolves
   // with vmcnt(0): the first key round then waited for the whole burst)
-  auto issue_dma = [&](const PlLayerPtrs& Ly) {
+  auto issue_dma = [&]() {
     if (dma_split) {
       if (w >= 4) {
 #pragma unroll
-        for (int m = 0; m < 18; ++m) dma_one(Ly, w + zz - 4 + 4 * m);
+        for (int m = 0; m < 18; ++m) dma_one(w - 4 + 4 * m);
       }
     } else {
 #pragma unroll
-      for (int m = 0; m < 9; ++m) dma_one(Ly, w + zz + 8 * m);
+      for (int m = 0; m < 9; ++m) dma_one(w + 8 * m);
     }
   };
-  // c_attn weight fragments of a layer (12 of 16 fragment columns real)
-  auto load_bw = [&](const PlLayerPtrs& Ly) {
-    const u32x4_t* wq = Ly.qkv_w12 + (int64_t)(b + zz) * 32 * 4 * kQC;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int s = w + 8 * i;
-      if constexpr (WKEEP || ITTS_PL_KEEP_QKV)
-        bw[i] = wq[(s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0)];
-      else
-        bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
-    }
-  };
-  // the attention's first round of K/V rows (pass 0) of a layer's cache
-  auto kv_round0 = [&](const uint16_t* kc_l, const uint16_t* vc_l) {
+  // the attention's first round of K/V rows (pass 0)
+  auto kv_round0 = [&]() {
     const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
     const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
     stage_kvi(rr, p0, nk);
-    kv_load(kr, kc_l, rr, p0, nk, 0);
-    kv_load(vr, vc_l, rr, p0, nk, 0);
+    kv_load(kr, p.kc, rr, p0, nk, 0);
+    kv_load(vr, p.vc, rr, p0, nk, 0);
   };
-  // x^ written inside this launch (phase G of the previous layer, write-through): sc1 loads
-  auto rsrc_xh = [&]() __attribute__((always_inline)) {
-    uint16_t* q = p.xh;
-    if constexpr (MULTI) asm volatile("" : "+s"(q));
-    return __builtin_amdgcn_make_buffer_rsrc(q, 0, 0x7fffffff, 0x00020000);
-  };
+  // x^ rows of the NEXT row tiles were written by the previous launch: plain buffer loads (sc1, as any hand-off)
+  const auto rsrc_xh = __builtin_amdgcn_make_buffer_rsrc(p.xh, 0, 0x7fffffff, 0x00020000);
   {
-    const u32x4_t* wq = p.ly[0].qkv_w12 + (int64_t)b * 32 * 4 * kQC;
+    const u32x4_t* wq = Ly.qkv_w12 + (int64_t)b * 32 * 4 * kQC;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s = w + 8 * i;
-      if constexpr (WKEEP || ITTS_PL_KEEP_QKV)
-        bw[i] = wq[(s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0)];
-      else
-        bw[i] = __builtin_nontemporal_load(wq + (s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0));
+      bw[i] = wq[(s * 4 + q4) * kQC + (c16 < kQC ? c16 : 0)];
 #pragma unroll
       for (int t = 0; t < NHF; ++t)
-        av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)a_row(0, 16 * t + c16) * kD + 32 * s + 8 * q4);
+        av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!ITTS_PL_KV_LATE) kv_round0(p.kc, p.vc);
-    if (ITTS_PL_DMA_EARLY) {
-      __builtin_amdgcn_sched_barrier(0);
-      issue_dma(p.ly[0]);
-    }
+    kv_round0();
   }
 
   // fold statistics of one 32-row tile (the A fragments a wave accumulated): sums -> mu / rstd in LDS
@@ -513,72 +414,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       fold_mu_rs(S, Q, 1.0f / kD, p.eps, mu[tid], rsd[tid]);
     }
   };
-
-  // ==== the launch's layers: layer li at epoch L1 = L1base + li.  Between two layers (the seam): every
-  // workgroup's phase G stores its x^ rows write-through and adds to CNT7; the next layer's c_attn weights and
-  // first K/V round are requested right after that add, and its x^ operands once the seam poll has matched.
-#pragma unroll 1
-  for (int li = 0; li < (MULTI ? p.nl : 1); ++li) {
-  const PlLayerPtrs& Ly = p.ly[li];
-  const uint32_t L1 = L1base + (uint32_t)li;
-  uint16_t* const kc = p.kc + (int64_t)li * p.layer_cache;
-  uint16_t* const vc = p.vc + (int64_t)li * p.layer_cache;
-  cur_layer = p.layer + li;
-  // the per-lane indices pass through an opaque copy each layer, so the compiler cannot hoist the dozens of
-  // lane addresses derived from them out of the loop (held across all layers they took every VGPR and spilled)
-  if (MULTI) {
-    asm volatile("" : "+v"(tid), "+v"(lane), "+v"(c16), "+v"(q4), "+v"(r32), "+v"(hb), "+v"(tu), "+v"(g), "+v"(d8),
-                 "+v"(xrow), "+v"(xcol));
-    // and an opaque zero that the uniform offsets (DMA sources, c_attn weights, K/V head offset) add, so they are
-    // not hoisted out of the loop either (they were, and spilled)
-    zz = 0;
-    asm volatile("" : "+s"(zz));
-    w = wave + zz;
-    u = w >> 2;
-    c = (b + zz) % kNC;
-    j = (b + zz) / kNC;
-    hh = j >> 4;
-    jj = j & 15;
-    h = 2 * c + hh;
-  }
-  if (MULTI && li > 0) {
-    mark(0);
-    if (w == 0 && lane < kNC) {  // lane q polls producer cluster q's counter for this cluster
-      const uint32_t* ctr = cnt_(CNT7 + kNC * lane + c);
-      const uint32_t target = kCPC * (L1 - 1u);
-      bool ok = true;
-      for (uint32_t n = 0;; ++n) {
-        if ((int32_t)(ld_relaxed(ctr) - target) >= 0) break;
-        if ((n & 255) == 255 && ld_relaxed(err_()) != 0) {
-          ok = false;
-          break;
-        }
-        if (n > kSpinMax) {
-          __hip_atomic_store(err_(), 7u, __ATOMIC_RELAXED, PL_SCOPE);
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (!ok) *abort_flag = 1;
-    }
-    bar();
-    if (*abort_flag) return;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int t = 0; t < NHF; ++t)
-        av[i][t] = __builtin_amdgcn_raw_buffer_load_b128(
-            rsrc_xh(), (a_row(0, 16 * t + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
-  }
   mark(1);
-  dbg(0, (uint32_t)kidx);
-  dbg(1, (uint32_t)(p.pad ? p.pad[0] : 0));
-  dbg(2, av[0][0][0]);
-  dbg(3, __float_as_uint(x_raw[0].x));
-  dbg(4, bw[0][0]);
-  dbg(5, kr[0][0]);
-  dbg(6, vr[0][0]);
 
   // ---- (A) c_attn per 32-row tile: decode_gemm16x FOLD arithmetic (k-steps w + 8i, statistics from the
   // A fragments); q / k / v of row r, head h -> granules gq[r][h][192]; this step's k / v into the cache
@@ -602,7 +438,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
           avn[i][hf] = __builtin_amdgcn_raw_buffer_load_b128(
-              rsrc_xh(), (a_row(t + 1, 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
+              rsrc_xh, ((32 * (t + 1) + 16 * hf + c16) * kD + 32 * (w + 8 * i) + 8 * q4) * 2, 0, PL_AUX);
     }
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
     float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
@@ -632,30 +468,27 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
     bar();
     if constexpr (MT > 1) {
       // several row tiles: the same outputs, but every store instruction issued by every wave (lanes with no
-      // output get an offset past the buffer's range: the hardware drops them), so the compiler counts the
-      // stores exactly and waits for the next tile's A fragments without waiting for these write-through stores
-      // (with lane-conditional stores its wait at the tile loop's head was vmcnt(0))
+      // output get the offset kDrop past the descriptor's range: the hardware drops them), so the compiler counts
+      // the stores exactly and waits for the next tile's A fragments without waiting for these write-through
+      // stores (with lane-conditional stores its wait at the tile loop's head was vmcnt(0))
       const int e = tid >> 6, l = lane, col = l & 15;
       const bool ok = col < kQC;
       const int cq = ok ? col : 0;
       float v = 0.f;
 #pragma unroll
       for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
-      const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = a_row(t, rt);
+      const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = 32 * t + rt;
       v = fold_apply(v, rsd[rt], mu[rt], uc0, uc1);
       const int i = kQC * jj + cq;
       const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
       const int goff = ok ? (((row * kH + h) * 192 + i) * 8) : kDrop;
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{(uint32_t)gr, (uint32_t)(gr >> 32)},
-                                            __builtin_amdgcn_make_buffer_rsrc(gq_(), 0, kDropLimit, 0x00020000), goff,
-                                            0, PL_AUX);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{(uint32_t)gr, (uint32_t)(gr >> 32)}, rsrc_lim(gq), goff, 0,
+                                            PL_AUX);
       const int coff = (row * (int)p.cache_bs + h * (int)p.cache_hs + kidx * kHD + (i & (kHD - 1))) * 2;
       const bool kv_ok = ok && row < R;
       const uint16_t hv = f2bf(0.f + v);
-      __builtin_amdgcn_raw_buffer_store_b16(hv, __builtin_amdgcn_make_buffer_rsrc(kc, 0, kDropLimit, 0x00020000),
-                                            kv_ok && i >= kHD && i < 2 * kHD ? coff : kDrop, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b16(hv, __builtin_amdgcn_make_buffer_rsrc(vc, 0, kDropLimit, 0x00020000),
-                                            kv_ok && i >= 2 * kHD ? coff : kDrop, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(hv, rsrc_lim(p.kc), kv_ok && i >= kHD && i < 2 * kHD ? coff : kDrop, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(hv, rsrc_lim(p.vc), kv_ok && i >= 2 * kHD ? coff : kDrop, 0, 0);
     } else {  // one output per thread: 32 rows x 16 fragment columns (12 real)
       const int e = tid >> 6, l = lane, col = l & 15;
       if (col < kQC) {
@@ -667,9 +500,9 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
         v = fold_apply(v, rsd[rt], mu[rt], uc[col], uc[kQC + col]);
         const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
         const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
-        __hip_atomic_store(gq_() + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, PL_SCOPE);
+        __hip_atomic_store(gq + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, PL_SCOPE);
         if (i >= kHD && row < R) {  // this step's key / value into the row's own cache row (0 + v, rounded)
-          uint16_t* dst = (i < 2 * kHD ? kc : vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
+          uint16_t* dst = (i < 2 * kHD ? p.kc : p.vc) + (int64_t)row * p.cache_bs + (int64_t)h * p.cache_hs +
                           (int64_t)kidx * kHD + (i & (kHD - 1));
           *dst = f2bf(0.f + v);
         }
@@ -683,7 +516,6 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
         for (int hf = 0; hf < 2; ++hf) av[i][hf] = avn[i][hf];
     }
   }
-  if (ITTS_PL_KV_LATE) kv_round0(kc, vc);  // pass 0's K/V rows behind the c_attn operands instead
   mark(2);
 
   // ---- (E1 + B) attention passes: unit u of pass pt = row 32 pt + 2 jj + u of head h (attn_decode_kernel
@@ -706,32 +538,28 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
     const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
     if (pt > 0) {  // later passes: this pass's first round now
       stage_kvi(rr, p0, nk);
-      kv_load(kr, kc, rr, p0, nk, 0);
-      kv_load(vr, vc, rr, p0, nk, 0);
+      kv_load(kr, p.kc, rr, p0, nk, 0);
+      kv_load(vr, p.vc, rr, p0, nk, 0);
     }
     if ((w & 3) == 0 && act_u) {  // the unit's first wave sweeps its 192 granules
-      const uint64_t* src = gq_() + ((int64_t)r_u * kH + h) * 192;
+      const uint64_t* src = gq + ((int64_t)r_u * kH + h) * 192;
       uint64_t g0, g1, g2;
       bool ok = false;
-      for (uint32_t n = 0;; ++n) {
+      for (uint32_t n = 0; !dead; ++n) {
         g0 = ld_sc1_u64(src + lane);
         g1 = ld_sc1_u64(src + 64 + lane);
         g2 = ld_sc1_u64(src + 128 + lane);
         const bool mine = (uint32_t)(g0 >> 32) == L1 && (uint32_t)(g1 >> 32) == L1 && (uint32_t)(g2 >> 32) == L1;
         if (__all(mine)) {
           ok = true;
-          if (ITTS_PL_ACQ) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
           break;
         }
-        if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err_()) != 0)) break;
+        if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err) != 0)) break;
         __builtin_amdgcn_s_sleep(1);
       }
       if (!ok) {
         if (lane == 0) {
-          __hip_atomic_store(err_(), 1u, __ATOMIC_RELAXED, PL_SCOPE);
+          if (!dead) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, PL_SCOPE);
           *abort_flag = 1;
         }
       } else {
@@ -742,17 +570,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
     }
     bar();
     if (pt == 0) mark(3);
-    if (pt == 0) {
-      dbg(7, __float_as_uint(qs[0]));
-      dbg(8, __float_as_uint(kn[0]));
-      dbg(9, __float_as_uint(vn[0]));
-    }
-    if (*abort_flag) return;
+    if (*abort_flag || dead) return;
     // the later phases' weights: behind the c_attn operands and this pass's K/V rows, after the q/k/v
     // granule sweep (a burst issued earlier queued in front of those loads: profiles/pl_trace_r04b.txt)
-    // ITTS_PL_DMA_LATE: the burst goes out after the first key round (its K/V rows, in flight since launch
-    // start, are then waited for on their own: behind an LDS-DMA the compiler can only emit vmcnt(0))
-    if (!ITTS_PL_DMA_EARLY && !ITTS_PL_DMA_LATE && pt == 0) issue_dma(Ly);
+    if (pt == 0) issue_dma();
     if (act_u) {
       float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       float m_run = -INFINITY, l_run = 0.f;
@@ -797,7 +618,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
           pt_ = sum8_dpp(pt_);
           sc[uu] = jk < nk ? pt_ : -INFINITY;
         }
-        if (more) kv_load(kr, kc, rr, p0, nk, j0 + NG * KB);
+        if (more) kv_load(kr, p.kc, rr, p0, nk, j0 + NG * KB);
 #pragma unroll
         for (int c0 = 0; c0 < KB; c0 += kSub) {
           float bm = -INFINITY;
@@ -825,56 +646,19 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
           }
           m_run = mn;
         }
-        if (more) kv_load(vr, vc, rr, p0, nk, j0 + NG * KB);
+        if (more) kv_load(vr, p.vc, rr, p0, nk, j0 + NG * KB);
       };
       key_round(0);  // nk >= 1: round 0 always runs
-      if (ITTS_PL_DMA_LATE && !ITTS_PL_DMA_EARLY && pt == 0) {
-        asm volatile("" ::: "memory");
-        issue_dma(Ly);
-      }
       if (pt == 0) mark(21);
-      // everything but the next round's 2 KB K/V rows (round 1 waits for the weight DMA whatever we do: the
-      // counter retires in order).  A compiler-visible wait: without it the DMA still pending at the loop's
-      // entry made the compiler's wait at the loop head vmcnt(0) in EVERY round (each round's V rows then
-      // waited for together with the next round's K rows; C3 step 642 -> 770 us when the layer loop came in)
-      // (small steps issue round 1 conditionally: there everything, round 1 included)
-      // (MULTI only: the single-layer form gets counted waits without it)
-      if constexpr (MULTI) __builtin_amdgcn_s_waitcnt(vm_wait_enc(ITTS_PL_KV_UNCOND && !H16 ? 2 * KB : 0));
       for (int j0 = NG * KB; j0 < nk; j0 += NG * KB) key_round(j0);
       if (pt == 0) mark(20);
-      if constexpr (SG) {
-        if (tu < 8) {  // lane group 0's copy of group g's partial -> [h][g]: o (64 f32), m, l (write-through)
-          const auto rp = rsrc_of(kOffPa);
-          const int base = ((h * 32 + g) * kPaStride) * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4_t{__float_as_uint(o8[0]), __float_as_uint(o8[1]), __float_as_uint(o8[2]), __float_as_uint(o8[3])},
-              rp, base + 32 * d8, 0, PL_AUX);
-          __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4_t{__float_as_uint(o8[4]), __float_as_uint(o8[5]), __float_as_uint(o8[6]), __float_as_uint(o8[7])},
-              rp, base + 32 * d8 + 16, 0, PL_AUX);
-          if (d8 == 0)
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(m_run), __float_as_uint(l_run)}, rp,
-                                                  base + 256, 0, PL_AUX);
-        }
-      } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
-        if (d8 == 0) {
-          gm[g] = m_run;
-          gl[g] = l_run;
-        }
+      for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[e];
+      if (d8 == 0) {
+        gm[g] = m_run;
+        gl[g] = l_run;
       }
     }
-    // (after the block, not as its else: the structurizer turns an else into a DMA block ahead of the
-    // attention, whose join then forces vmcnt(0) on the active units' first key round)
-    if (ITTS_PL_DMA_LATE && !ITTS_PL_DMA_EARLY && pt == 0) {
-      // an opaque copy of !act_u: with the plain condition the compiler turns this into the else of the
-      // attention block, laid out ahead of it, and the join makes the active units' first wait vmcnt(0)
-      int idle = !act_u;
-      asm volatile("" : "+v"(idle)::"memory");
-      if (idle) issue_dma(Ly);
-    }
-    if constexpr (!SG) {
     bar();
     if (act_u) {
       const int dd = tu & (kHD - 1), qd = tu / kHD;
@@ -911,45 +695,22 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(kOffOb), ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, PL_AUX);
     }
-    }  // !SG
     if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
   mark(4);
-  dbg(10, obf[0]);
   drain();  // the o stores, and this wave's weight DMA (read from LDS from phase C on)
   bar();
   mark(15);
   if (tid == 0) add_relaxed(cnt_(CNT2 + c));
 
   // ---- (C) attn.c_proj split c, tile j, per 32-row tile: decode_gemm_kernel EPI 2 (one k-step per wave)
-  if (tid == 0 && !poll_ge(cnt_(CNT2 + c), kCPC * L1, err_(), 2)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT2 + c), kCPC * L1, err, 2)) *abort_flag = 1;
   mark(5);
   bar();
   if (*abort_flag) return;
-  // 1024 outputs of row tile t, fixed-order sum over the waves; ITTS_PL_PART16=1: 4 consecutive
-  // columns per thread as ONE 16-B write-through store (256 threads) instead of 4-B stores (512 x 2; A/B, off:
-  // measured neutral, profiles/lib_ab2.sh): a
-  // narrow sc1 store is one fabric write each (MI355X_MICROARCH.md visibility table: dword ~6x the
-  // dwordx4 time per byte), and the drain before the counter add waits for all of them
+  // 1024 outputs of row tile t, fixed-order sum over the waves, 4-B write-through stores (16-B stores gathered
+  // over 4 lanes measured neutral)
   auto store_partial = [&](float* dst, int t) {
-    if (ITTS_PL_PART16) {
-      if (tid < 256) {
-        const int o = 4 * tid;
-        float v4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ww = 0; ww < kNW; ++ww)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v4[k] += red[ww * 1024 + o + k];
-        const int r = o >> 6, l = o & 63;
-        const int row = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
-        const u32x4_t pv4{__float_as_uint(v4[0]), __float_as_uint(v4[1]), __float_as_uint(v4[2]),
-                          __float_as_uint(v4[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(pv4, rs, (((c * kMaxR + row) * kD) + 32 * j + (l & 31)) * 4, 0,
-                                               PL_AUX);
-      }
-      return;
-    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int o = tid + 512 * k;
@@ -965,56 +726,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   {
     const u32x4_t bb = *reinterpret_cast<const u32x4_t*>(lds_wo + w * 1024 + lane * 16);
     u32x4_t ao[MT];  // every row tile's o fragment requested up front (4 VGPRs a tile)
-    if constexpr (SG) {
-      // the cluster's two heads' 32 group partials -> LDS (red), then row 0's o from them in the in-unit merge's
-      // order: M = max m; per quarter of 8 groups L_q, a_q by fmaf in group order; L = sum L_q, a = sum a_q; o = a / L
-      const auto rp = rsrc_of(kOffPa);
-      constexpr int NV = 2 * 32 * kPaStride / 4, NPT = (NV + kThreads - 1) / kThreads;  // 16-B vectors
-      u32x4_t pt4[NPT];  // every load issued before the first LDS write (one round trip, not NPT)
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) {
-        const int v = tid + kThreads * k;
-        if (v < NV) pt4[k] = __builtin_amdgcn_raw_buffer_load_b128(rp, (2 * c * 32 * kPaStride) * 4 + 16 * v, 0, PL_AUX);
-      }
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) {
-        const int v = tid + kThreads * k;
-        if (v < NV) reinterpret_cast<u32x4_t*>(red)[v] = pt4[k];
-      }
-      bar();
-      u32x4_t a = u32x4_t{0u, 0u, 0u, 0u};
-      if (r32 == 0) {  // row 0 (the one row), this lane's 8 of the cluster's 128 dims
-        const int kk = 16 * w + 8 * hb, d0 = kk & (kHD - 1);
-        const float* P = red + (kk >> 6) * 32 * kPaStride;
-        float M = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) M = fmaxf(M, P[i * kPaStride + 64]);
-        float Ls = 0.f, at[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int qd = 0; qd < NQ; ++qd) {
-          float Lq = 0.f, aq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
-            const float wgt = __expf(P[i * kPaStride + 64] - M);
-            Lq = fmaf(P[i * kPaStride + 65], wgt, Lq);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) aq[e] = fmaf(P[i * kPaStride + d0 + e], wgt, aq[e]);
-          }
-          Ls += Lq;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) at[e] += aq[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] = pack2bf(at[2 * e] / Ls, at[2 * e + 1] / Ls);
-      }
-      bar();  // red is the MFMA epilogue's next
-      ao[0] = a;
-    } else {
 #pragma unroll
     for (int t = 0; t < MT; ++t)
       ao[t] = __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(kOffOb),
                                                     ((c * kMaxR + 32 * t + r32) * 128 + 16 * w + 8 * hb) * 2, 0, PL_AUX);
-    }
 #pragma unroll  // (MT > 1: straight-line tiles, so the compiler's vmcnt counts stay exact across them)
     for (int t = 0; t < MT; ++t) {
       const u32x4_t a = ao[t];
@@ -1026,7 +741,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
 #pragma unroll
       for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
       bar();
-      store_partial(p1_(), t);
+      store_partial(p1, t);
       bar();
     }
   }
@@ -1037,7 +752,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   if (tid == 0) add_relaxed(cnt_(CNT3 + j));
 
   // ---- (D) x1 = x + (b_o + sum_c partial_c) on tile j (residual_reduce_ln_v4 order), x1^ -> cluster copy
-  if (tid == 0 && !poll_ge(cnt_(CNT3 + j), kNC * L1, err_(), 3)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT3 + j), kNC * L1, err, 3)) *abort_flag = 1;
   mark(7);
   bar();
   if (*abort_flag) return;
@@ -1050,21 +765,13 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       float2 pp = ob2;
 #pragma unroll
       for (int cc = 0; cc < kNC; ++cc) {
-        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p1_() + ((int64_t)cc * kMaxR + row) * kD + xcol));
+        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p1 + ((int64_t)cc * kMaxR + row) * kD + xcol));
         pp.x += __uint_as_float((uint32_t)v);
         pp.y += __uint_as_float((uint32_t)(v >> 32));
       }
       const float2 xo = row < R ? x_raw[t] : float2{0.f, 0.f};
       x1[t] = float2{xo.x + pp.x, xo.y + pp.y};
-      const uint32_t pk = pack2bf(x1[t].x, x1[t].y);
-      if (ITTS_PL_XC16) {  // 8 columns (4 lanes) per 16-B write-through store (a 4-B sc1 store is one fabric write)
-        const uint32_t n1 = __shfl_down(pk, 1, 64), n2 = __shfl_down(pk, 2, 64), n3 = __shfl_down(pk, 3, 64);
-        if ((lane & 3) == 0)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{pk, n1, n2, n3}, rsrc_of(kOffXc),
-                                                 ((c * kMaxR + row) * kD + xcol) * 2, 0, PL_AUX);
-      } else {
-        st_sc1_u32(reinterpret_cast<uint32_t*>(xc() + (((int64_t)c * kMaxR + row) * kD + xcol) * 2), pk);
-      }
+      st_sc1_u32(reinterpret_cast<uint32_t*>(xc + (((int64_t)c * kMaxR + row) * kD + xcol) * 2), pack2bf(x1[t].x, x1[t].y));
     }
   }
   mark(8);
@@ -1074,11 +781,10 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   if (tid == 0) add_relaxed(cnt_(CNT4 + c));
 
   // ---- (E) c_fc (ln_2 folded) + gelu on column tile 32c + j, per row tile, A = the cluster's x1^
-  if (tid == 0 && !poll_ge(cnt_(CNT4 + c), kCPC * L1, err_(), 4)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT4 + c), kCPC * L1, err, 4)) *abort_flag = 1;
   // past this poll every workgroup of the grid has added at E3 (cluster c's 32 E4 adders each waited for
   // the 8 clusters of its tile), so all have read the epoch: workgroup 0 advances it for the next launch
-  // (the next launch starts at epoch L1base + nl)
-  if (li == 0 && b == 0 && tid == 0 && !*abort_flag) st_sc1_u32(seq, L1base + (uint32_t)(p.nl - 1));
+  if (b == 0 && tid == 0 && !*abort_flag) st_sc1_u32(seq, L1);
   mark(9);
   bar();
   if (*abort_flag) return;
@@ -1139,8 +845,8 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
         const int rt = lane >> 1, half = lane & 1;
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + rt * 16 + 8 * half);
         __builtin_amdgcn_raw_buffer_store_b128(
-            v, rsrc_of_lim(kOffFc), w == 0 ? ((c * kMaxR + 32 * t + rt) * 512 + 16 * j + 8 * half) * 2 : kDrop, 0,
-            PL_AUX);
+            v, rsrc_lim(p.scratch + kOffFc), w == 0 ? ((c * kMaxR + 32 * t + rt) * 512 + 16 * j + 8 * half) * 2 : kDrop,
+            0, PL_AUX);
       } else if (tid < 64) {  // [32 rows][16 columns] bf16 -> the cluster's f tile, write-through 16-B stores
         const int rt = tid >> 1, half = tid & 1;
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + rt * 16 + 8 * half);
@@ -1163,7 +869,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   if (tid == 0) add_relaxed(cnt_(CNT5 + c));
 
   // ---- (F) mlp.c_proj split c, tile j, per row tile: decode_gemm_kernel EPI 2 (k-steps w + 8i of the split)
-  if (tid == 0 && !poll_ge(cnt_(CNT5 + c), kCPC * L1, err_(), 5)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT5 + c), kCPC * L1, err, 5)) *abort_flag = 1;
   mark(11);
   bar();
   if (*abort_flag) return;
@@ -1191,7 +897,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
 #pragma unroll
       for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc32[r];
       bar();
-      store_partial(p2_(), t);
+      store_partial(p2, t);
       bar();
       if (MT > 1) {
 #pragma unroll
@@ -1205,27 +911,22 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
   mark(19);
   if (tid == 0) add_relaxed(cnt_(CNT6 + j));
 
-  // ---- (G) x2 = x1 + (b_proj + sum_c partial_c) on tile j.  Wave c (rows 4c .. 4c+3 of every tile) stores x^
-  // for the next layer (write-through: the seam) and, at the launch's end, x; inside the launch every wave keeps
-  // its rows' x2 as the next layer's residual slices.  The model's last layer stores x1 and leaves this reduce
-  // (with ln_f + final_norm, Q5) to itts_residual_reduce_ln over the partials.  Every layer adds to the seam
-  // counters (each CNT7 counter holds 32 x the epoch after it).
-  const bool more_layers = MULTI && li + 1 < p.nl;
-  if (p.last && !more_layers) {
+  // ---- (G) x2 = x1 + (b_proj + sum_c partial_c) on tile j: wave c (rows 4c .. 4c+3 of every tile) stores x and
+  // x^ for the next launch.  The model's last layer stores x1 and leaves this reduce (with ln_f + final_norm, Q5)
+  // to itts_residual_reduce_ln over the partials.
+  if (p.last) {
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int row = 32 * t + xrow;
       if ((xrow >> 2) == c && row < R) *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x1[t];
     }
-    if (p.seam && w == 0 && lane < kNC) add_relaxed(cnt_(CNT7 + kNC * c + lane));
     return;
   }
-  if (tid == 0 && !poll_ge(cnt_(CNT6 + j), kNC * L1, err_(), 6)) *abort_flag = 1;
+  if (tid == 0 && !poll_ge(cnt_(CNT6 + j), kNC * L1, err, 6)) *abort_flag = 1;
   mark(13);
   bar();
   if (*abort_flag) return;
-  // x2 of this wave's rows (4w .. 4w+3 of every row tile) -> x_raw; wave c stores them
-  auto g_rows = [&](bool store) __attribute__((always_inline)) {
+  if (w == c) {
     const float2 pb2 = *reinterpret_cast<const float2*>(Ly.proj_b + xcol);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
@@ -1234,54 +935,45 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgsT<MULTI ? 
       float2 pp = pb2;
 #pragma unroll
       for (int cc = 0; cc < kNC; ++cc) {
-        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p2_() + ((int64_t)cc * kMaxR + row) * kD + xcol));
+        const uint64_t v = ld_sc1_u64(reinterpret_cast<const uint64_t*>(p2 + ((int64_t)cc * kMaxR + row) * kD + xcol));
         pp.x += __uint_as_float((uint32_t)v);
         pp.y += __uint_as_float((uint32_t)(v >> 32));
       }
       const float2 x2 = float2{x1[t].x + pp.x, x1[t].y + pp.y};
-      x_raw[t] = x2;
-      if (store) {
-        if (!more_layers) *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x2;
-        const uint32_t pk = pack2bf(x2.x, x2.y);
-        if (MULTI) {  // 8 columns (4 lanes) per 16-B write-through store: a narrow sc1 store is one fabric write
-          const uint32_t n1 = __shfl_down(pk, 1, 64), n2 = __shfl_down(pk, 2, 64), n3 = __shfl_down(pk, 3, 64);
-          if ((lane & 3) == 0)
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{pk, n1, n2, n3}, rsrc_xh(), (row * kD + xcol) * 2, 0, PL_AUX);
-        } else {
-          *reinterpret_cast<uint32_t*>(p.xh + (int64_t)row * kD + xcol) = pk;
-        }
-      }
+      *reinterpret_cast<float2*>(p.x + (int64_t)row * kD + xcol) = x2;
+      *reinterpret_cast<uint32_t*>(p.xh + (int64_t)row * kD + xcol) = pack2bf(x2.x, x2.y);
     }
-  };
-  if (w == c) g_rows(true);
-  if (MULTI) {
-    if (w == c) drain();  // the x^ stores (write-through) have left before the seam add
-    bar();
   }
-  if ((MULTI || p.seam) && w == 0 && lane < kNC) add_relaxed(cnt_(CNT7 + kNC * c + lane));
   mark(14);
-  if (more_layers) {
-    // the other waves' residual rows for the next layer (off the seam's critical path: after the add), then the
-    // next layer's c_attn weights and first K/V round, in flight across the seam
-    if (w != c) g_rows(false);
-    load_bw(p.ly[li + 1]);
-    if (!ITTS_PL_KV_LATE) kv_round0(kc + p.layer_cache, vc + p.layer_cache);
-  }
-  }  // layers
 }
 
+// occupancy of the instantiations the default path launches, per row-tile count MT (both the plain and the
+// lineage form: a caller of itts_gpt_pl_supported need not say whether the state has beams) and the small-step
+// form: each must fit one workgroup per CU (LDS, registers), the grid being one workgroup per CU.  -1: not
+// queried yet.
 int g_cu_count = -1;
-// layers 0 .. n-1 read ALL their weights with the default cache policy (WKEEP), so they can stay in the Infinity
-// Cache between steps: C3 decode step 657.7-657.9 us with none, 653.1-653.5 with 4, 652.7-654.4 with 8,
-// 663.8-664.0 with 12 (profiles/r05e_batch1.txt).  Since every layer's c_attn operands are read that way
-// (ITTS_PL_KEEP_QKV: 126 MB, the launch head's critical path) none is best: 646.0-646.9 vs 646.1-649.9 with 4
-// (C2 505.9 vs 508.6-510.6).  ITTS_PL_KEEP_LAYERS overrides (default 0)
-int keep_layers() {
-  static const int n = [] {
-    const char* e = getenv("ITTS_PL_KEEP_LAYERS");
-    return e ? atoi(e) : 0;
-  }();
-  return n;
+int g_occ[5] = {-1, -1, -1, -1, -1};  // [0]: the small-step form; [MT]: MT row tiles
+
+template <typename K>
+int fits(K k) {
+  int nb = 0;
+  const bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k), kThreads, 0) ==
+                  hipSuccess && nb >= 1;
+  (void)hipGetLastError();
+  return ok ? 1 : 0;
+}
+
+int occ_ok(int slot) {
+  if (g_occ[slot] < 0) {
+    switch (slot) {
+      case 0: g_occ[0] = fits(gpt_layer_pl_kernel<1, false, kKBSmall, kSmallH16>); break;
+      case 1: g_occ[1] = fits(gpt_layer_pl_kernel<1, false>) & fits(gpt_layer_pl_kernel<1, true>); break;
+      case 2: g_occ[2] = fits(gpt_layer_pl_kernel<2, false>) & fits(gpt_layer_pl_kernel<2, true>); break;
+      case 3: g_occ[3] = fits(gpt_layer_pl_kernel<3, false>) & fits(gpt_layer_pl_kernel<3, true>); break;
+      default: g_occ[4] = fits(gpt_layer_pl_kernel<4, false>) & fits(gpt_layer_pl_kernel<4, true>); break;
+    }
+  }
+  return g_occ[slot];
 }
 
 }  // namespace
@@ -1294,28 +986,15 @@ extern "C" int itts_gpt_pl_supported(const ItTsGptWeights* w, int rows) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       n = 0;
-    // every instantiation must fit one workgroup per CU (LDS, registers): the grid is one per CU
-    int occ = 1;
-    const void* ks[] = {reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, true>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, false>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<4, true>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKB, false, false, true>),
-                        reinterpret_cast<const void*>(gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, true>),
-                        reinterpret_cast<const void*>(
-                            gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, false, kSmallH16>)};
-    for (const void* k : ks) {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess || nb < 1) occ = 0;
-    }
     (void)hipGetLastError();
-    g_cu_count = occ ? n : 0;
+    g_cu_count = n;
   }
   // every workgroup must be resident at once (one per CU); the caller must also keep other work off the
   // device's CUs while a layer runs: a workgroup that cannot be placed makes the
   // resident ones time out (itts_gpt_pl_error), never hang
-  return g_cu_count >= kWG ? 1 : 0;
+  if (g_cu_count < kWG) return 0;
+  const int mt = (rows + 31) / 32;
+  return occ_ok(mt) && (rows > kSmallRows || occ_ok(0)) ? 1 : 0;
 }
 
 extern "C" int itts_gpt_pl_error(const void* scratch, void* stream, int* code) {
@@ -1332,33 +1011,6 @@ extern "C" int itts_gpt_pl_error(const void* scratch, void* stream, int* code) {
 }
 
 namespace {
-// layers per persistent launch (ITTS_PL_LPL; default 1 = one launch per layer).  The multi-layer form (layers
-// joined inside the launch by the CNT7 seam, the next layer's c_attn weights and first K/V round requested across
-// it) is bit-identical and measured SLOWER: C3 decode step 714 vs 647 us, C2 547 vs 513 us (profiles/
-// pl_trace_r05o_lpl*.txt): the seam (x2 reduce by one wave, 16-B write-through x^ stores, drain, 8 x 8 replicated
-// counters, poll, 64 KiB of x^ per workgroup read back from the memory side) costs more than the kernel boundary
-// it replaces (G -> next layer's operands issued: 5.8 vs 3.8 us)
-int layers_per_launch() {
-  static const int n = [] {
-    const char* e = getenv("ITTS_PL_LPL");
-    const int v = e ? atoi(e) : 1;
-    return v < 1 ? 1 : (v > kMaxLpl ? kMaxLpl : v);
-  }();
-  return n;
-}
-
-// one-row steps with the split softmax groups (SG, opt-in A/B: ITTS_PL_SPLITG=1): bit-identical, measured slower,
-// C2 step 604 vs 500 us (profiles/pl_trace_r05x_sg{0,1}.txt): the attention ends ~2 us earlier, but the E2 drain then
-// waits for the layer's weight DMA (no long attention to hide it any more) and phase C's serial 32-group merge in
-// 16 lanes takes 4.2 us
-bool split_groups() {
-  static const bool on = [] {
-    const char* e = getenv("ITTS_PL_SPLITG");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 PlLayerPtrs layer_ptrs(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl) {
   PlLayerPtrs q;
   q.qkv_w12 = static_cast<const u32x4_t*>(pl->qkv_w12);
@@ -1378,20 +1030,19 @@ bool layer_ok(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl) {
          ly->proj_b && ly->o_c;
 }
 
-// layers layer .. layer + nl - 1 (weights ly[0 .. nl-1]) of decode step kstep as ONE launch
-int launch_layers(const ItTsGptLayerW* const* lyw, const ItTsGptPlLayerW* const* plw, const ItTsGptDecodeState* st,
-                  int layer, int nl, int kstep, int last, bool keep, void* scratch, hipStream_t s, const char* fn) {
+// layer `layer` of decode step kstep as ONE launch
+int launch_layer(const ItTsGptLayerW* lyw, const ItTsGptPlLayerW* plw, const ItTsGptDecodeState* st, int layer,
+                 int kstep, int last, void* scratch, hipStream_t s, const char* fn) {
   const int64_t cache_hs = (int64_t)st->max_kv * kHD, cache_bs = (int64_t)kH * cache_hs;
   const int64_t layer_cache = (int64_t)st->rows * cache_bs;
-  PlArgsT<kMaxLpl> a;
-  for (int i = 0; i < nl; ++i) a.ly[i] = layer_ptrs(lyw[i], plw[i]);
+  PlArgs a;
+  a.ly = layer_ptrs(lyw, plw);
   a.x = st->x;
   a.xh = static_cast<uint16_t*>(st->xh);
   a.kc = static_cast<uint16_t*>(st->k_cache) + layer * layer_cache;
   a.vc = static_cast<uint16_t*>(st->v_cache) + layer * layer_cache;
   a.cache_bs = cache_bs;
   a.cache_hs = cache_hs;
-  a.layer_cache = layer_cache;
   a.pad = st->pad;
   a.tstate = st->tstate;
   a.kv_rows = st->kv_rows;
@@ -1400,55 +1051,38 @@ int launch_layers(const ItTsGptLayerW* const* lyw, const ItTsGptPlLayerW* const*
   a.kstep = kstep;
   a.R = st->rows;
   a.layer = layer;
-  a.nl = nl;
   a.last = last;
-  a.seam = layers_per_launch() > 1;  // CNT7 counts stay n x epoch only if every launch of the process adds
   a.eps = 1e-5f;
   a.scratch = static_cast<unsigned char*>(scratch);
-  PlArgsT<1> a1;
-  static_cast<PlCommon&>(a1) = a;
-  a1.ly[0] = a.ly[0];
   const int mt = (st->rows + 31) / 32;
   const int ki = 2 * (mt - 1) + (st->kv_rows ? 1 : 0);
   if (ki == 0 && st->rows <= kSmallRows) {  // kSmallRows <= 16: one 16-row half
-    if (nl > 1)
-      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, true>), dim3(kWG), dim3(kThreads), 0,
-                         s, a);
-    else if (st->rows == 1 && kSmallH16 && split_groups())
-      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16, false, kSmallH16>), dim3(kWG),
-                         dim3(kThreads), 0, s, a1);
-    else if (keep)
-      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, true, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s, a1);
-    else
-      hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, false, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s,
-                         a1);
-    return itts::check_launch(fn);
-  }
-  if (ki == 0 && keep) {
-    hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKB, true>), dim3(kWG), dim3(kThreads), 0, s, a1);
-    return itts::check_launch(fn);
-  }
-  if (ki == 0 && nl > 1) {
-    hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKB, false, false, true>), dim3(kWG), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s, a);
     return itts::check_launch(fn);
   }
   switch (ki) {
-    case 0: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
-    case 1: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
-    case 2: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
-    case 3: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
-    case 4: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
-    case 5: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
-    case 6: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, false>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
-    default: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, true>), dim3(kWG), dim3(kThreads), 0, s, a1); break;
+    case 0: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, false>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    default: hipLaunchKernelGGL((gpt_layer_pl_kernel<4, true>), dim3(kWG), dim3(kThreads), 0, s, a); break;
   }
   return itts::check_launch(fn);
 }
 
 int check_state(const ItTsGptDecodeState* st, void* scratch, const char* fn) {
   ITTS_REQUIRE(st->rows >= 1 && st->rows <= kMaxR, fn, "1..128 rows");
+  ITTS_REQUIRE(st->max_kv >= 1, fn, "max_kv >= 1");
   ITTS_REQUIRE(!st->kv_rows || st->ld_rows >= st->max_kv, fn, "kv_rows [rows][ld_rows >= max_kv]");
   ITTS_REQUIRE(!st->kv_rows || st->max_kv <= kKviMax, fn, "beam states: max_kv <= 3584 on the persistent path");
+  // the K/V stores of row tiles > 1 are cancellable buffer stores (range kDropLimit, int32 byte offsets): every
+  // real offset into one layer's cache, R x 16 heads x max_kv x 64 x 2 B, must lie below kDropLimit (beyond it a
+  // real store would be dropped silently)
+  ITTS_REQUIRE((int64_t)st->rows * kH * st->max_kv * kHD * 2 < (int64_t)kDropLimit, fn,
+               "K/V cache of one layer must be < 2 GiB - 64 KiB (rows x max_kv <= 1,048,543)");
   ITTS_REQUIRE(st->x && st->xh && st->k_cache && st->v_cache && st->tstate, fn, "null state buffer");
   ITTS_REQUIRE((reinterpret_cast<uintptr_t>(scratch) & 255) == 0, fn, "scratch must be 256-B aligned");
   return 0;
@@ -1461,8 +1095,7 @@ extern "C" int itts_gpt_layer_pl(const ItTsGptLayerW* ly, const ItTsGptPlLayerW*
   ITTS_REQUIRE(ly && pl && st && scratch, fn, "null pointer");
   ITTS_REQUIRE(layer_ok(ly, pl), fn, "incomplete layer weights");
   if (int rc = check_state(st, scratch, fn)) return rc;
-  return launch_layers(&ly, &pl, st, layer, 1, kstep, last, layer < keep_layers(), scratch, itts::as_stream(stream),
-                       fn);
+  return launch_layer(ly, pl, st, layer, kstep, last, scratch, itts::as_stream(stream), fn);
 }
 
 // Re-arm the scratch: counters, every granule, the epoch and the error word to zero.  An ordinary kernel
@@ -1504,25 +1137,10 @@ extern "C" int itts_gpt_decode_steps_pl(const ItTsGptWeights* w, const ItTsGptPl
   const int L = w->n_layer, D = w->d_model, R = st->rows;
   if (int rc = check_state(st, scratch, fn)) return rc;
   for (int l = 0; l < L; ++l) ITTS_REQUIRE(layer_ok(&w->layers[l], &pl[l]), fn, "incomplete layer weights");
-  // the step's layers in launches of up to layers_per_launch() (the keep-policy layers in launches of their own)
-  const ItTsGptLayerW* lyw[kMaxLpl];
-  const ItTsGptPlLayerW* plw[kMaxLpl];
-  const int nkeep = keep_layers();
-  const int lpl = (R <= 32 && !st->kv_rows) ? layers_per_launch() : 1;
   hipStream_t s = itts::as_stream(stream);
   int rc = 0;
   for (int k = 0; k < nsteps && rc == 0; ++k) {
-    for (int l0 = 0; l0 < L && rc == 0;) {
-      const bool keep = l0 < nkeep;
-      int nl = L - l0 < lpl ? L - l0 : lpl;
-      if (keep && l0 + nl > nkeep) nl = nkeep - l0;
-      for (int i = 0; i < nl; ++i) {
-        lyw[i] = &w->layers[l0 + i];
-        plw[i] = &pl[l0 + i];
-      }
-      rc = launch_layers(lyw, plw, st, l0, nl, k, l0 + nl == L, keep, scratch, s, fn);
-      l0 += nl;
-    }
+    for (int l = 0; l < L && rc == 0; ++l) rc = launch_layer(&w->layers[l], &pl[l], st, l, k, l + 1 == L, scratch, s, fn);
     // the last layer's mlp.c_proj reduce with ln_f + final_norm (Q5) over the persistent partials
     if (rc == 0)
       rc = itts_residual_reduce_ln(st->x, D, reinterpret_cast<float*>(static_cast<unsigned char*>(scratch) + kOffP2),

@@ -3,6 +3,14 @@
 //   BigVGAN/models.py:192,246-248 ; infer.py:627-631,658
 // Channel-last input [B][Tmax][C] (bf16 or f32). One thread per output sample; the [256+6][C] input
 // window of a workgroup is staged once through LDS as f32.
+//
+// itts_act_conv_post_tanh (round 6): activation_post (Activation1d, models.py:245) fused in front -- the
+// vocoder's last AMP stage output is read once and the 24-channel activation output (629 MB per C3 batch)
+// never goes to HBM.  Bit-identical to itts_aa_snakebeta_fwd (bf16, MFMA path) + itts_conv_post_tanh: the
+// activation strips start at multiples of 32 samples as the activation kernel's do (the MFMA sums depend on
+// the strip alignment), edge outputs use the same exact formula, the rounded bf16 activation values feed the
+// same conv loop in the same order.
+#include "act_mfma.h"
 #include "common.h"
 
 namespace {
@@ -39,7 +47,148 @@ __global__ __launch_bounds__(256) void conv_post_tanh_kernel(const TI* __restric
     pcm[(int64_t)b * syb + t] = (int16_t)s;  // C cast truncates toward zero, like torch .type(int16)
   }
 }
+
+// ---- activation_post + conv_post + tanh (+ int16) ----
+constexpr int kApTiles = 16;               // activation output tiles per job: 4 waves x 4
+constexpr int kApTO = 32 * kApTiles - 64;  // conv outputs per job: 448; activation rows [t0 - 32, t0 + 480)
+constexpr int kApWin = 32 * kApTiles + 32; // window rows: times t0 - 39 .. t0 + 504 (replicate-clamped)
+constexpr int kApPX = 64;                  // window row bytes: one 32-channel block (C <= 32)
+constexpr int kApKMax = 15;                // conv taps (odd, halo K / 2 <= 7 < 32)
+constexpr int kApLds = kApWin * kApPX + 128 + 32 * kApKMax * 4 + 32 * kApTiles * 32 * 2;
+
+struct ApArgs {
+  const uint16_t* x;
+  int64_t sxb, ldx;
+  const float *up, *down, *log_alpha, *log_beta;
+  const float* w;  // conv_post [C][K]
+  float bias;
+  int C, K;
+  const int32_t* lens;
+  int T;
+  float* wav;
+  int16_t* pcm;
+  int64_t syb;
+};
+
+__global__ __launch_bounds__(256, 2) void act_post_conv_kernel(ApArgs p) {
+  constexpr int PX = kApPX;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* win = smem;                                            // [kApWin][64] bf16 window
+  float* tl = reinterpret_cast<float*>(smem + kApWin * PX);             // 12 up, 12 down taps
+  float* wl = tl + 32;                                                  // conv_post [C][K]
+  uint16_t* at = reinterpret_cast<uint16_t*>(wl + 32 * kApKMax);        // activation rows [512][C] bf16
+  const int b = blockIdx.y;
+  const int len = p.lens ? p.lens[b] : p.T;
+  const int t0 = blockIdx.x * kApTO;
+  if (t0 >= len) return;
+  const int ta0 = t0 - 32;  // time of activation row 0 (a multiple of 32, like the activation kernel's strips)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = p.C, K = p.K;
+  if (tid < 24) tl[tid] = tid < 12 ? p.up[tid] : p.down[tid - 12];
+  for (int i = tid; i < C * K; i += 256) wl[i] = p.w[i];
+  // window row r = time ta0 - 7 + r (clamped to [0, len)), channels >= C zero: the activation kernel's window
+  const uint16_t* X = p.x + (int64_t)b * p.sxb;
+  constexpr int NV = (kApWin * 4 + 255) / 256;
+  u32x4_t buf[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = tid + 256 * i;
+    const int r = v >> 2, c = (v & 3) * 8;
+    const int t = min(max(ta0 - 7 + r, 0), len - 1);
+    buf[i] = (v < kApWin * 4 && c < C) ? ld_stream(reinterpret_cast<const u32x4_t*>(X + (int64_t)t * p.ldx + c))
+                                       : u32x4_t{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = tid + 256 * i;
+    if (v < kApWin * 4) *reinterpret_cast<u32x4_t*>(win + itts_actm::woff<PX>(v >> 2, (v & 3) * 8)) = buf[i];
+  }
+  __syncthreads();
+  // activation strips (act.hip aa_snake_mfma_kernel, NB = 1): wave w -> rows [128 w, 128 w + 128)
+  {
+    itts_actm::Taps T;
+    itts_actm::make_taps(tl, T);
+    const int ch = lane & 31, h = lane >> 5;
+    const float a_rev = ch < C ? expf(p.log_alpha[ch]) * 0.15915494309189535f : 0.f;
+    const float inv_b = ch < C ? 1.0f / (expf(p.log_beta[ch]) + 1e-9f) : 0.f;
+    const int ts = ta0 + wave * 128;
+    const int ntile = min(4, max(0, (len - ts + 31) / 32));
+    itts_actm::strip<PX>(win, wave * 128, 0, ntile, T, a_rev, inv_b, [&](int i, const f32x16_t& acc) {
+      const int t = ts + 32 * i + (lane & 31);
+      if (t < 3 || t >= len - 3) return;  // edges (and rows outside [0, len)): below
+      uint16_t* ar = at + (t - ta0) * C + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (8 * g + 4 * h < C) {
+          const u32x2_t o{pack2bf(acc[4 * g], acc[4 * g + 1]), pack2bf(acc[4 * g + 2], acc[4 * g + 3])};
+          *reinterpret_cast<u32x2_t*>(ar + 8 * g) = o;
+        }
+      }
+    });
+  }
+  // rows within 3 samples of an utterance edge: the exact formula; rows outside [0, len): the conv's zeros
+  if (ta0 < 3 || ta0 + 32 * kApTiles > len - 3) {
+    for (int it = tid; it < 32 * kApTiles * C; it += 256) {
+      const int r = it / C, cc = it - r * C;
+      const int t = ta0 + r;
+      if (t >= 3 && t < len - 3) continue;
+      float v = 0.f;
+      if (t >= 0 && t < len) {
+        const float a = expf(p.log_alpha[cc]) * 0.15915494309189535f;
+        const float ib = 1.0f / (expf(p.log_beta[cc]) + 1e-9f);
+        v = itts_actm::exact_at<PX>(win, ta0 - 7, t, len, cc, tl, a, ib);
+      }
+      at[r * C + cc] = f2bf(v);
+    }
+  }
+  __syncthreads();
+  // conv_post + tanh (+ int16): conv_post_tanh_kernel's loop order over the bf16 activation rows
+  const int half = K / 2;
+  for (int o = tid; o < kApTO; o += 256) {
+    const int t = t0 + o;
+    if (t >= len) break;
+    float acc = p.bias;
+    for (int j = 0; j < K; ++j) {
+      const uint16_t* row = at + (t - half + j - ta0) * C;
+      for (int c8 = 0; c8 < C; c8 += 8) {
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(row + c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t wv = v[e >> 1];
+          const float xv = __uint_as_float((e & 1) ? (wv & 0xFFFF0000u) : (wv << 16));
+          acc = fmaf(wl[(c8 + e) * K + j], xv, acc);
+        }
+      }
+    }
+    const float v = tanhf(acc);
+    if (p.wav) p.wav[(int64_t)b * p.syb + t] = v;
+    if (p.pcm) {
+      const float s = fminf(fmaxf(32767.0f * v, -32767.0f), 32767.0f);
+      p.pcm[(int64_t)b * p.syb + t] = (int16_t)s;
+    }
+  }
+}
 }  // namespace
+
+extern "C" int itts_act_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* up12, const float* down12,
+                                       const float* log_alpha, const float* log_beta, const float* w, float bias, int C,
+                                       int K, const int32_t* lengths, int B, int Tmax, float* wav, int16_t* pcm,
+                                       int64_t y_sb, void* stream) {
+  const char* fn = "itts_act_conv_post_tanh";
+  ITTS_REQUIRE(B >= 0 && Tmax >= 0 && C > 0 && K > 0, fn, "bad sizes");
+  if (B == 0 || Tmax == 0) return 0;
+  ITTS_REQUIRE(x && up12 && down12 && log_alpha && log_beta && w && (wav || pcm), fn, "null pointer");
+  ITTS_REQUIRE(C % 8 == 0 && C <= 32, fn, "C must be a multiple of 8, at most 32 (one MFMA channel block)");
+  ITTS_REQUIRE((K & 1) && K <= kApKMax, fn, "K must be odd and at most 15");
+  ITTS_REQUIRE(ldx % 8 == 0 && x_sb % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0, fn,
+               "channel-last bf16 rows must be 16-B aligned");
+  ApArgs a{static_cast<const uint16_t*>(x), x_sb, ldx, up12, down12, log_alpha, log_beta, w, bias, C, K, lengths, Tmax,
+           wav, pcm, y_sb};
+  dim3 grid((Tmax + kApTO - 1) / kApTO, B);
+  hipLaunchKernelGGL(act_post_conv_kernel, grid, dim3(256), kApLds, itts::as_stream(stream), a);
+  return itts::check_launch(fn);
+}
+
 
 // w: f32 [C][K] (conv_post weight [1, C, K] squeezed), bias: scalar.
 extern "C" int itts_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx, const float* w, float bias, int C, int K,

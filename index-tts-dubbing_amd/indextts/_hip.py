@@ -40,10 +40,10 @@ SIGNATURES = {
                               _c_i, _c_i, _c_i, _i32p, _c_i, _c_i, _c_f, _c_i, _c_i, _vp]),
     "itts_amp_conv_fwd": (_c_i, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp,
                                  _c_i, _c_i, _c_i, _c_i, _c_i, _i32p, _c_f, _vp]),
-    "itts_amp_conv_act_fwd": (_c_i, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i, _c_i, _c_i, _c_i,
-                                     _c_i, _i32p, _vp, _vp, _vp, _vp, _vp]),
     "itts_conv_post_tanh":(_c_i, [_vp, _c_i64, _c_i64, _vp, _c_f, _c_i, _c_i, _vp, _c_i, _c_i, _vp, _vp, _c_i64,
                                    _c_i, _vp]),
+    "itts_act_conv_post_tanh": (_c_i, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_f, _c_i, _c_i, _vp, _c_i, _c_i,
+                                       _vp, _vp, _c_i64, _vp]),
     "itts_log_mel": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _vp, _c_i, _c_i, _c_i, _vp, _vp]),
     "itts_resample_sinc": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _c_i, _c_i, _c_i, _vp, _c_i64, _c_i, _vp]),
     "itts_igemm_splitk": (_c_i, [_vp, _c_i64, _c_i, _c_i, _vp, _c_i, _c_i, _vp, _vp, _vp, _vp]),

@@ -214,6 +214,9 @@ class HipGPT:
         # key count becomes the DISTINCT (cache row, position) pairs its beams read (bench.py roofline)
         self.beam_lineage = None
         self.logits_trace = None  # set to a list to record every step's raw logits [B, V] (tests)
+        # set to a list to record every beam step's state after its selection (tests): one step per replay, then
+        # (codes [R, steps], beam scores [R], utterances done [B]) on the host
+        self.beam_trace = None
         # algorithmic HBM bytes of one decode step: every weight byte once (+ per-key KV bytes)
         eb = 2 if dtype == "bf16" else 4
         self.step_weight_bytes = sum(eb * ly.w[n]["N"] * ly.w[n]["K"] for ly in self.layers for n in ly.w) \
@@ -535,6 +538,7 @@ class HipGPT:
     # PL_MAX_BEAM_ROWS: beam3's 96-row step 1330 us vs 1360 on the chain (profiles/r05_b3pl.sh r05u)
     PL_MAX_ROWS = int(os.environ.get("ITTS_PL_MAX_ROWS", "128"))
     PL_MAX_BEAM_ROWS = int(os.environ.get("ITTS_PL_MAX_BEAM_ROWS", "96"))
+    BEAM_MAX_KV = 3584  # kKviMax of gpt_attn.hip / gpt_layer.hip (lineage indices staged in LDS)
 
     @property
     def pl_active(self):
@@ -556,14 +560,14 @@ class HipGPT:
         """persistent layers for this state: <= PL_MAX_ROWS (<= 128) rows, a 256-CU device with room for one
         workgroup per CU, not held off, and no other lane of this engine decoding concurrently (two
         persistent grids could each hold part of the CUs)"""
-        cap = max(self.PL_MAX_ROWS, self.PL_MAX_BEAM_ROWS) if st.get("kv_rows") is not None else self.PL_MAX_ROWS
+        cap = self.PL_MAX_BEAM_ROWS if st.get("kv_rows") is not None else self.PL_MAX_ROWS
         return (self.pl_active and st["B"] <= min(cap, 128) and not st.get("multi_lane", False)
                 and bool(self.lib.itts_gpt_pl_supported(ctypes.byref(self._cweights), st["B"])))
 
     def pl_takes(self, rows: int, beams: bool = False) -> bool:
         """would a decode of ``rows`` rows (beam states: utterances x num_beams) run on the persistent layers
         (no lane split, within the row cap, supported on this device)"""
-        cap = max(self.PL_MAX_ROWS, self.PL_MAX_BEAM_ROWS) if beams else self.PL_MAX_ROWS
+        cap = self.PL_MAX_BEAM_ROWS if beams else self.PL_MAX_ROWS
         if not (self.pl_active and 0 < rows <= min(cap, 128)):
             return False
         if not beams and len(self._lane_bounds(rows, None)) > 1:
@@ -594,13 +598,19 @@ class HipGPT:
         if off:
             self.pl = False
 
+    TRACES = ("step_events", "logits_trace", "beam_lineage", "beam_trace")
+
     def _with_pl_fallback(self, fn, *args, **kw):
         self._pl_ran = False
+        # the instrumentation lists' lengths: a re-run replaces what the failed attempt recorded
+        marks = {k: len(getattr(self, k)) for k in self.TRACES if getattr(self, k) is not None}
         out = fn(*args, **kw)
         if self._pl_ran:
             code = self.pl_error()
             if code:
                 self._pl_recover(code)
+                for k, n in marks.items():
+                    del getattr(self, k)[n:]
                 with self.launch_chain():
                     out = fn(*args, **kw)
         return out
@@ -1071,6 +1081,9 @@ class HipGPT:
         -> codes [B, n] int64 (best hypothesis, then the stop token, padded with it)."""
         K = int(num_beams)
         assert 2 <= K <= 16, "num_beams must be in [2, 16]"
+        if self.max_kv > self.BEAM_MAX_KV:  # both beam attentions stage the lineage rows of a key range in LDS
+            raise ValueError(f"beam decoding supports a KV capacity of at most {self.BEAM_MAX_KV} positions "
+                             f"(this engine: max_kv={self.max_kv}); build the engine with a smaller max_kv")
         if do_sample and seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         return self._with_pl_fallback(self._generate_beam, conds, text_ids, max_new_tokens, K, repetition_penalty,
@@ -1121,6 +1134,13 @@ class HipGPT:
         else:
             self._dgw(st["h"], self.head_w, R, self.head_b, st["logits"])
         self._beam_step(st, 0)
+        btr = self.beam_trace
+
+        def trace_step(n_done):
+            btr.append((st["codes"][:, :n_done].cpu(), st["beam_score"].cpu(), st["done_u"].cpu()))
+
+        if btr is not None:
+            trace_step(1)
         gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep, self.pl_active)
         graph_ok = use_graph and max_new_tokens > 1
         if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
@@ -1130,7 +1150,7 @@ class HipGPT:
         # distinct cache keys a step reads: each utterance's prompt once (shared by its beams through
         # the lineage table) + every beam row's generated keys
         keys0 = int(B * (s + 1) - int(pad.sum())) if ev is not None else 0
-        kmulti = self.GRAPH_STEPS if graph_ok else 1
+        kmulti = self.GRAPH_STEPS if graph_ok and btr is None else 1
         while steps < max_new_tokens:
             n = kmulti if (kmulti > 1 and steps + kmulti <= max_new_tokens
                            and (steps % check_every) + kmulti <= check_every) else 1
@@ -1152,6 +1172,8 @@ class HipGPT:
                     ev.append((e0 if j == 0 else e1, e1, R, keys0 + R * (steps + j)))
             prev = steps
             steps += n
+            if btr is not None:
+                trace_step(steps)
             if steps // check_every != prev // check_every and bool(st["done_u"].all()):
                 break
         if ev is not None and self.beam_lineage is not None:  # resolved by the caller, outside its timed region

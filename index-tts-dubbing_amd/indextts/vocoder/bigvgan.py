@@ -140,13 +140,8 @@ class HipBigVGAN:
     # act (vocoder 101 ms; act fused into the conv for 24 / 48: 107 ms);  others: act + igemm
     FUSED_CHANNELS = ()
     SPLIT_CHANNELS = (24, 48, 96)
-    # round 5: conv1 -> act2 of a layer in one launch (itts_amp_conv_act_fwd: the conv output's HBM round trip
-    # gone, bit-identical).  Measured NOT faster (profiles/ubench_epi_r05.txt: C = 48 at parity, C = 24 up to
-    # 14 % slower than conv + activation kernel: the fused tile runs the activation's MFMA chains after the
-    # conv's at 3 waves per SIMD), so off by default; ITTS_VOC_EPI="24,48" turns it on (A/B)
-    EPI_CHANNELS = ()
-    if os.environ.get("ITTS_VOC_EPI") is not None:
-        EPI_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_EPI"].split(",") if v)
+    # (round 5 also built conv1 -> act2 of a layer as one launch: bit-identical, measured not faster --
+    # profiles/ubench_epi_r05.txt -- and removed in round 6)
     if os.environ.get("ITTS_VOC_FUSED") is not None:  # tuning sweeps: "24,48,96"
         FUSED_CHANNELS = tuple(int(v) for v in os.environ["ITTS_VOC_FUSED"].split(",") if v)
         SPLIT_CHANNELS = tuple(sorted({24, 48, 96} - set(FUSED_CHANNELS)))
@@ -232,7 +227,7 @@ class HipBigVGAN:
         if self.fused_amp and C in self.FUSED_CHANNELS:
             return 1
         if self.fused_amp and C in self.SPLIT_CHANNELS:
-            return 3 if C in self.EPI_CHANNELS else 2
+            return 2
         return 0
 
     def _c_weights(self):
@@ -326,14 +321,6 @@ class HipBigVGAN:
             y.data_ptr(), Ty * y.shape[2], y.shape[2], lens.data_ptr(), B, T, Cin, c.cout, c.ntaps, c.offs,
             float(alpha), _hip.stream_ptr()), "itts_amp_conv_fwd")
 
-    def _amp_act(self, c: _Conv, x, y, lens, a: _Act):
-        """y = act(conv(x) + bias) in one launch (itts_amp_conv_act_fwd): conv1 -> act2 of a layer."""
-        B, T, Cin = x.shape
-        _hip.check(self.lib.itts_amp_conv_act_fwd(
-            x.data_ptr(), T * Cin, Cin, c.w.data_ptr(), c.bias.data_ptr(), y.data_ptr(), y.shape[1] * y.shape[2],
-            y.shape[2], lens.data_ptr(), B, T, Cin, c.cout, c.ntaps, c.offs, a.up.data_ptr(), a.down.data_ptr(),
-            a.alpha.data_ptr(), a.beta.data_ptr(), _hip.stream_ptr()), "itts_amp_conv_act_fwd")
-
     def _conv(self, c: _Conv, x, y, lens, r1=None, r2=None, alpha=1.0, bias_b=None, ymul=1, yoff=0, Tq=None):
         B, T, Cin = x.shape
         Ty = y.shape[1]
@@ -418,10 +405,6 @@ class HipBigVGAN:
                     if fused:  # activation fused into each conv's input staging (amp_conv.hip)
                         self._amp(c1, src, t2, lens_n, a1)
                         self._amp(c2, t2, dst, lens_n, a2, r1=src, r2=r2, alpha=alpha)
-                    elif split and C in self.EPI_CHANNELS:  # act kernel, conv1 -> act2 in one launch, conv2
-                        self._act(a1, src, t1, lens_n)
-                        self._amp_act(c1, t1, t2, lens_n, a2)
-                        self._amp(c2, t2, dst, lens_n, r1=src, r2=r2, alpha=alpha)
                     elif split:  # activation kernel + the all-channels conv kernel without activation
                         self._act(a1, src, t1, lens_n)
                         self._amp(c1, t1, t2, lens_n)
@@ -436,12 +419,31 @@ class HipBigVGAN:
             cur_in, Tcur, lens = xs, Tn, lens_n
             if taps is not None:
                 taps[f"stage{i}"], taps[f"stage{i}_lens"] = xs.clone(), lens_n.clone()
-        t1 = self._buf("t1", cur_in.shape)
-        self._act(self.act_post, cur_in, t1, lens)
         wav = torch.empty(B, Tcur, dtype=torch.float32, device=dev)
         pcm = torch.empty(B, Tcur, dtype=torch.int16, device=dev) if want_pcm else None
-        C = t1.shape[2]
-        _hip.check(self.lib.itts_conv_post_tanh(
-            t1.data_ptr(), Tcur * C, C, self.post_w.data_ptr(), self.post_b, C, self.post_k, lens.data_ptr(), B, Tcur,
-            wav.data_ptr(), _hip.ptr(pcm), Tcur, _hip.dtype_code(t1), _hip.stream_ptr()), "itts_conv_post_tanh")
+        self._tail(cur_in, lens, wav, pcm)
         return wav, pcm
+
+    def tail_fused(self, x) -> bool:
+        """activation_post + conv_post + tanh (+ int16) as one launch (itts_act_conv_post_tanh): bf16 channel-last
+        input of 8..32 channels (one MFMA channel block; IndexTTS-1.5: 24), the layout the generator runs in"""
+        C = x.shape[2]
+        return (x.dtype == torch.bfloat16 and C % 8 == 0 and C <= 32 and self.post_k % 2 == 1 and self.post_k <= 15
+                and os.environ.get("ITTS_VOC_TAIL_FUSED", "1") != "0")
+
+    def _tail(self, x, lens, wav, pcm, fused=None):
+        """wav / pcm = tanh(conv_post(activation_post(x))) (models.py:245-248; int16 as infer.py:627-631):
+        one fused launch (bit-identical, tests/test_gpu_vocoder.py), or the activation kernel + itts_conv_post_tanh"""
+        B, T, C = x.shape
+        if fused if fused is not None else self.tail_fused(x):
+            a = self.act_post
+            _hip.check(self.lib.itts_act_conv_post_tanh(
+                x.data_ptr(), T * C, C, a.up.data_ptr(), a.down.data_ptr(), a.alpha.data_ptr(), a.beta.data_ptr(),
+                self.post_w.data_ptr(), self.post_b, C, self.post_k, lens.data_ptr(), B, T, wav.data_ptr(),
+                _hip.ptr(pcm), wav.shape[1], _hip.stream_ptr()), "itts_act_conv_post_tanh")
+            return
+        t1 = self._buf("t1", x.shape)
+        self._act(self.act_post, x, t1, lens)
+        _hip.check(self.lib.itts_conv_post_tanh(
+            t1.data_ptr(), T * C, C, self.post_w.data_ptr(), self.post_b, C, self.post_k, lens.data_ptr(), B, T,
+            wav.data_ptr(), _hip.ptr(pcm), wav.shape[1], _hip.dtype_code(t1), _hip.stream_ptr()), "itts_conv_post_tanh")

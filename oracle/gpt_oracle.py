@@ -35,8 +35,12 @@ def _f32(sd: Dict[str, object]) -> Dict[str, torch.Tensor]:
 
 
 class GPTOracle:
-    def __init__(self, sd, cfg_gpt):
+    def __init__(self, sd, cfg_gpt, sd_decode=None):
+        """``sd``: the weights every pass uses; ``sd_decode`` (optional): other weights for the KV-cached
+        decode steps only (tests: the bf16 product path stores its prefill and decode GEMM weights
+        differently -- rounded W vs rounded diag(ln.g) W, tests/parity_util.py ``bf16_effective_gpt_sds``)."""
         self.sd = _f32(sd)
+        self.sd_dec = self.sd if sd_decode is None else _f32(sd_decode)
         g = cfg_gpt
         self.D, self.L, self.H = int(g.model_dim), int(g.layers), int(g.heads)
         self.hd = self.D // self.H
@@ -64,8 +68,8 @@ class GPTOracle:
         return emb, mask
 
     # ---------------- GPT-2 core ----------------
-    def _block(self, i, x, kv, attn_bias):
-        sd, H, hd = self.sd, self.H, self.hd
+    def _block(self, i, x, kv, attn_bias, sd=None):
+        sd, H, hd = sd if sd is not None else self.sd, self.H, self.hd
         p = f"gpt.h.{i}"
         B, T, D = x.shape
         h = F.layer_norm(x, (D,), sd[p + ".ln_1.weight"], sd[p + ".ln_1.bias"], 1e-5)
@@ -83,13 +87,14 @@ class GPTOracle:
         f = F.gelu(torch.addmm(sd[p + ".mlp.c_fc.bias"], h.reshape(-1, D), sd[p + ".mlp.c_fc.weight"]), approximate="tanh")
         return x + torch.addmm(sd[p + ".mlp.c_proj.bias"], f, sd[p + ".mlp.c_proj.weight"]).view(B, T, D)
 
-    def core(self, x, attn_bias, kv=None):
+    def core(self, x, attn_bias, kv=None, sd=None):
+        sd = self.sd if sd is None else sd
         for i in range(self.L):
-            x = self._block(i, x, kv, attn_bias)
-        return F.layer_norm(x, (self.D,), self.sd["gpt.ln_f.weight"], self.sd["gpt.ln_f.bias"], 1e-5)
+            x = self._block(i, x, kv, attn_bias, sd)
+        return F.layer_norm(x, (self.D,), sd["gpt.ln_f.weight"], sd["gpt.ln_f.bias"], 1e-5)
 
-    def head(self, h):
-        sd = self.sd
+    def head(self, h, sd=None):
+        sd = self.sd if sd is None else sd
         h = F.layer_norm(h, (self.D,), sd["final_norm.weight"], sd["final_norm.bias"], 1e-5)
         return F.linear(h, sd["mel_head.weight"], sd["mel_head.bias"])
 
@@ -143,8 +148,8 @@ class GPTOracle:
             mask = torch.cat([mask, torch.ones(B, 1, dtype=mask.dtype)], 1)
             pos = mask.shape[1] - s  # quirk Q1: position j+1 for the j-th fed-back token (j >= 1)
             e = sd["mel_embedding.weight"][nxt] + sd["mel_pos_embedding.emb.weight"][pos]
-            h = self.core(e[:, None], self._bias(mask, 1), kv)
-            logits = self.head(h[:, -1])
+            h = self.core(e[:, None], self._bias(mask, 1), kv, self.sd_dec)
+            logits = self.head(h[:, -1], self.sd_dec)
         codes = torch.stack(out, 1)
         return (codes, trace) if return_trace else codes
 
@@ -171,7 +176,7 @@ class GPTOracle:
     def generate_beam(self, conds, text_ids, max_new_tokens: int, num_beams: int = 3,
                       repetition_penalty: float = 10.0, length_penalty: float = 0.0, min_new_tokens: int = 0,
                       do_sample: bool = False, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
-                      generator: Optional[torch.Generator] = None):
+                      generator: Optional[torch.Generator] = None, copies: int = 1, trace: Optional[list] = None):
         """``generate(num_beams=K)`` as transformers 4.36 runs it for ``inference_speech``
         (gpt/model.py:698-703): ``beam_search`` (do_sample=False) or ``beam_sample`` (do_sample=True)
         with ``BeamSearchScorer`` (HF:generation/beam_search.py process / finalize, BeamHypotheses
@@ -189,6 +194,12 @@ class GPTOracle:
         * an utterance is done once it holds K hypotheses and its worst one >= best candidate score /
           generated_len ** length_penalty; at max length the open beams are added as hypotheses.
         -> codes [B, n]: the best hypothesis per utterance, then the stop token (eos), padded with it.
+
+        Test conveniences (no effect on the semantics): ``copies`` decodes every utterance ``copies`` times
+        as independent utterances (b * copies + i; the prompt is prefilled once -- a row's prefill does not
+        depend on the other rows -- for sampling statistics); ``trace`` (a list) receives one entry per step
+        after its selection: the beams' sequences [R] and scores [B, K] and the step's 2K candidate scores
+        [B, 2K] (ranked as the selection saw them; their K-th vs K+1-th gap is the step's tie margin).
         """
         emb, mask = self.prepare_inputs(conds, text_ids)
         B, s, D = emb.shape
@@ -200,10 +211,11 @@ class GPTOracle:
         x = torch.cat([emb, start.expand(B, 1, D)], 1)
         kv: List[Optional[tuple]] = [None] * self.L
         h = self.core(x, self._bias(mask, s + 1), kv)
-        rows = torch.arange(B).repeat_interleave(K)  # row b*K + k <- utterance b
+        rows = torch.arange(B).repeat_interleave(K * copies)  # row b*K + k <- utterance b
         kv = [(k[rows], v[rows]) for k, v in kv]
         mask = mask[rows]
         logits = self.head(h[:, -1])[rows]
+        B = B * copies
         R = B * K
         seen = torch.zeros(R, V, dtype=torch.bool)
         seen[:, 1] = True
@@ -272,13 +284,16 @@ class GPTOracle:
             seqs = [seqs[int(parent[r])] + [int(token[r])] for r in range(R)]
             seen[torch.arange(R), token] = True
             beam_scores = new_scores
+            if trace is not None:
+                trace.append({"seqs": [list(q) for q in seqs], "scores": beam_scores.clone(), "vals": vals.clone(),
+                              "done": list(done)})
             if step == max_new_tokens - 1:
                 break
             mask = torch.cat([mask, torch.ones(R, 1, dtype=mask.dtype)], 1)
             pos = mask.shape[1] - s  # quirk Q1
             e = sd["mel_embedding.weight"][token] + sd["mel_pos_embedding.emb.weight"][pos]
-            h = self.core(e[:, None], self._bias(mask, 1), kv)
-            logits = self.head(h[:, -1])
+            h = self.core(e[:, None], self._bias(mask, 1), kv, self.sd_dec)
+            logits = self.head(h[:, -1], self.sd_dec)
         for b in range(B):  # finalize
             if done[b]:
                 continue
@@ -296,7 +311,9 @@ class GPTOracle:
 
     def forced_logits(self, conds, text_ids, codes: torch.Tensor):
         """Teacher-forced decode: the logits (after penalty) the generate loop sees at each step when
-        fed ``codes`` -> [B, n, V]. Lets fixtures compare per-step logits without free-running drift."""
+        fed ``codes`` -> [B, n, V]. Lets fixtures compare per-step logits without free-running drift.
+        (With ``sd_decode``: the prompt block through ``sd``, the fed codes through ``sd_decode`` over the
+        prompt's KV cache -- one causal chunk, the same values as one step at a time.)"""
         emb, mask = self.prepare_inputs(conds, text_ids)
         B, s, D = emb.shape
         sd = self.sd
@@ -306,10 +323,18 @@ class GPTOracle:
         pos = torch.tensor([0] + list(range(2, n + 1)))  # positions 0, 2, 3, ... (Q1)
         tok = codes[:, : n - 1]
         e = sd["mel_embedding.weight"][tok] + sd["mel_pos_embedding.emb.weight"][pos[1:n]][None]
-        full = torch.cat([x, e], 1)
         mask_full = torch.cat([mask, torch.ones(B, n - 1, dtype=mask.dtype)], 1)
-        h = self.core(full, self._bias(mask_full, full.shape[1]))
-        return self.head(h[:, s:])
+        if self.sd_dec is self.sd:
+            full = torch.cat([x, e], 1)
+            h = self.core(full, self._bias(mask_full, full.shape[1]))
+            return self.head(h[:, s:])
+        kv: List[Optional[tuple]] = [None] * self.L
+        h0 = self.core(x, self._bias(mask, s + 1), kv)[:, -1:]
+        out = [self.head(h0)]
+        if n > 1:
+            h1 = self.core(e, self._bias(mask_full, n - 1), kv, self.sd_dec)
+            out.append(self.head(h1, self.sd_dec))
+        return torch.cat(out, 1)
 
     # ---------------- post-processing + latent pass ----------------
     @staticmethod

@@ -56,3 +56,37 @@ def record(key, **values):
 def rel_rms(got, ref):
     got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
     return float(np.sqrt(np.mean((got - ref) ** 2) / np.mean(ref ** 2)))
+
+
+def bf16_effective_gpt_sds(sd, n_layer, rounding=True):
+    """The GPT weights as the bf16 product path stores them, as two f32 state dicts for
+    ``GPTOracle(sd_prefill, cfg, sd_decode=...)``, so that an oracle run on them differs from the GPU only by
+    activation rounding and summation order:
+
+      * prefill / latent GEMMs (itts_igemm_fwd over ``pack_taps``): bf16(W) of c_attn / attn.c_proj / mlp.c_fc /
+        mlp.c_proj, LayerNorms as they are;
+      * decode steps (itts_decode_gemm16x / the persistent layer, engine.fold_ln_weights -> itts_gpt_fold_ln,
+        gpt_pack.hip:32-56): ln_1 / ln_2 folded into c_attn / c_fc -- W' = bf16(f32(diag(g) W)) and the bias
+        c = b^T W + bias (double sums), applied behind an affine-free LayerNorm (rstd (x W' - mu 1^T W') + c is
+        LN(x) W' + c exactly) -- attn.c_proj / mlp.c_proj bf16(W);
+      * mel_head bf16(W) in both; embeddings, biases, ln_f / final_norm f32 (they are f32 on the device).
+    ``rounding=False``: the same folding without the bf16 rounding (a CPU test checks the fold is exact).
+    """
+    base = {k: torch.as_tensor(np.asarray(v)).float().clone() for k, v in sd.items()}
+    r16 = (lambda t: t.float().to(torch.bfloat16).float()) if rounding else (lambda t: t.float())  # noqa: E731
+    pre, dec = dict(base), dict(base)
+    for i in range(n_layer):
+        p = f"gpt.h.{i}"
+        for k in ("attn.c_attn", "attn.c_proj", "mlp.c_fc", "mlp.c_proj"):
+            pre[f"{p}.{k}.weight"] = r16(base[f"{p}.{k}.weight"])
+        for ln, k in (("ln_1", "attn.c_attn"), ("ln_2", "mlp.c_fc")):
+            g, b = base[f"{p}.{ln}.weight"].double(), base[f"{p}.{ln}.bias"].double()
+            w = base[f"{p}.{k}.weight"].double()  # HF Conv1D [in, out]
+            dec[f"{p}.{k}.weight"] = r16((w * g[:, None]).float())
+            dec[f"{p}.{k}.bias"] = (b @ w + base[f"{p}.{k}.bias"].double()).float()
+            dec[f"{p}.{ln}.weight"] = torch.ones_like(base[f"{p}.{ln}.weight"])
+            dec[f"{p}.{ln}.bias"] = torch.zeros_like(base[f"{p}.{ln}.bias"])
+        for k in ("attn.c_proj", "mlp.c_proj"):
+            dec[f"{p}.{k}.weight"] = r16(base[f"{p}.{k}.weight"])
+    pre["mel_head.weight"] = dec["mel_head.weight"] = r16(base["mel_head.weight"])
+    return pre, dec

@@ -135,34 +135,6 @@ def test_activation_kernel_c96_whole_row_jobs_equal_block_jobs(monkeypatch):
     assert bad.numel() == 0, (bad[:8].tolist(), lens.tolist())
 
 
-@pytest.mark.parametrize("C", [24, 32, 48, 96, 128])
-def test_activation_kernel_16b_stores_equal_8b_stores(monkeypatch, C):
-    """Interior outputs leave as 16-B stores (lanes n and n + 32 swap channel halves, ITTS_ACT_ST16=1) or as
-    the accumulator's 8-B quarters (default): the same values in the same places, ragged lengths included
-    (every channel-block count: NB = 1, 2, 3, 4)."""
-    from indextts.utils.synthetic import kaiser_sinc_lowpass
-    _hip, lib = _lib()
-    B, T = 12, 1100
-    g = torch.Generator().manual_seed(C + 7)
-    lens = torch.randint(1, T + 1, (B,), generator=g, dtype=torch.int32)
-    lens[0], lens[1], lens[2] = T, 1, 5
-    x = (torch.randn(B, T, C, generator=g) * 1.5).to(torch.bfloat16).cuda()
-    f = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).cuda()
-    la, lb = (torch.randn(C, generator=g) * 0.5).cuda(), (torch.randn(C, generator=g) * 0.5).cuda()
-    lensd = lens.cuda()
-    out = []
-    for st16 in ("1", "0"):
-        monkeypatch.setenv("ITTS_ACT_ST16", st16)
-        y = torch.full((B, T, C), -12352.0, dtype=torch.bfloat16, device="cuda")
-        _hip.check(lib.itts_aa_snakebeta_fwd(x.data_ptr(), y.data_ptr(), f.data_ptr(), f.data_ptr(), la.data_ptr(),
-                                             lb.data_ptr(), lensd.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1,
-                                             _hip.BF16, _hip.BF16, _hip.stream_ptr()), "fwd")
-        torch.cuda.synchronize()
-        out.append(y.view(torch.int16).cpu())
-    bad = (out[0] != out[1]).nonzero()
-    assert bad.numel() == 0, (bad[:8].tolist(), lens.tolist())
-
-
 @pytest.mark.parametrize("C,B,T", [(24, 160, 3000), (768, 64, 700), (192, 48, 1500), (96, 24, 2100)])
 def test_activation_kernel_mfma_persistent_many_jobs(C, B, T):
     """The MFMA activation kernel is persistent (each workgroup walks several (utterance, time tile)
@@ -505,41 +477,42 @@ def test_convtranspose_phases_as_output_columns_matches_torch(ci, co, k, u):
         assert bool((y[b, L * u:] == 9.0).all())
 
 
-@pytest.mark.parametrize("C,k,d,T,lens", [(24, 11, 5, 700, [700, 225, 224, 5, 1, 11]),
-                                          (24, 3, 1, 450, [450, 224, 231, 7, 2]),
-                                          (48, 7, 3, 700, [700, 448, 449, 3, 230]),
-                                          (48, 11, 1, 300, [300, 13, 6, 224])])
-def test_amp_conv_act_epilogue_equals_conv_then_activation(C, k, d, T, lens):
-    """itts_amp_conv_act_fwd (conv1 -> act2 of an AMPBlock1 layer in one launch, the activation run on the conv
-    tile in LDS) is BIT-identical to itts_amp_conv_fwd (no residuals, alpha 1) followed by the activation
-    kernel on its bf16 output: ragged lengths around the 224-row tile edges, utterances shorter than the
-    activation's 3-sample edge zones, every BigVGAN narrow-stage kernel size / dilation."""
+@pytest.mark.parametrize("C,K", [(24, 7), (8, 3), (16, 15), (32, 7)])
+def test_fused_tail_equals_activation_then_conv_post(C, K):
+    """itts_act_conv_post_tanh (activation_post -> conv_post -> tanh -> int16 in one launch, round 6) is
+    BIT-identical to itts_aa_snakebeta_fwd (bf16, MFMA path) followed by itts_conv_post_tanh on its bf16 output:
+    wav and pcm, ragged lengths around the 448-sample job edges and the 32-sample activation tiles, utterances
+    shorter than the activation's 3-sample edge zones (1, 2, 5, 6, 7 samples)."""
     from indextts.utils.synthetic import kaiser_sinc_lowpass
-    from indextts.vocoder.bigvgan import _Conv, conv1d_taps
     _hip, lib = _lib()
-    torch.manual_seed(C * k + d + T)
-    B = len(lens)
-    lens_t = torch.tensor(lens, dtype=torch.int32).cuda()
-    x = torch.randn(B, T, C).to(torch.bfloat16).cuda()
-    conv = _Conv(*conv1d_taps(torch.randn(C, C, k) / (C * k) ** 0.5, d), torch.randn(C) * 0.1, C, C, "cuda")
+    g = torch.Generator().manual_seed(C * 31 + K)
+    T = 2000
+    lens = torch.tensor([T, 1, 2, 5, 6, 7, 447, 448, 449, 896, 897, 31, 33, 1343, 1345, 1999], dtype=torch.int32)
+    B = lens.numel()
+    x = (torch.randn(B, T, C, generator=g) * 1.5).to(torch.bfloat16).cuda()
     up = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).float().cuda()
-    down = torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).float().cuda() * 1.01
-    la, lb = (torch.randn(C) * 0.3).cuda(), (torch.randn(C) * 0.3).cuda()
+    down = (torch.from_numpy(kaiser_sinc_lowpass(0.25, 0.3, 12)).reshape(-1).float() * 1.01).cuda()
+    la, lb = (torch.randn(C, generator=g) * 0.5).cuda(), (torch.randn(C, generator=g) * 0.5).cuda()
+    w = (torch.randn(C, K, generator=g) / (C * K) ** 0.5).cuda()
+    bias = 0.03
+    ld = lens.cuda()
     s = _hip.stream_ptr()
-    t2 = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
-    want = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
-    _hip.check(lib.itts_amp_conv_fwd(x.data_ptr(), T * C, C, None, None, None, None, conv.w.data_ptr(),
-                                     conv.bias.data_ptr(), None, None, t2.data_ptr(), T * C, C, lens_t.data_ptr(), B, T,
-                                     C, C, conv.ntaps, conv.offs, 1.0, s), "amp_conv")
-    _hip.check(lib.itts_aa_snakebeta_fwd(t2.data_ptr(), want.data_ptr(), up.data_ptr(), down.data_ptr(), la.data_ptr(),
-                                         lb.data_ptr(), lens_t.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1,
-                                         _hip.BF16, _hip.BF16, s), "act")
-    got = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
-    _hip.check(lib.itts_amp_conv_act_fwd(x.data_ptr(), T * C, C, conv.w.data_ptr(), conv.bias.data_ptr(), got.data_ptr(),
-                                         T * C, C, lens_t.data_ptr(), B, T, C, C, conv.ntaps, conv.offs, up.data_ptr(),
-                                         down.data_ptr(), la.data_ptr(), lb.data_ptr(), s), "amp_conv_act")
+    t1 = torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda")
+    _hip.check(lib.itts_aa_snakebeta_fwd(x.data_ptr(), t1.data_ptr(), up.data_ptr(), down.data_ptr(), la.data_ptr(),
+                                         lb.data_ptr(), ld.data_ptr(), B, C, T, T * C, C, 1, T * C, C, 1, _hip.BF16,
+                                         _hip.BF16, s), "act")
+    want_w = torch.full((B, T), 7.0, device="cuda")
+    want_p = torch.full((B, T), 123, dtype=torch.int16, device="cuda")
+    _hip.check(lib.itts_conv_post_tanh(t1.data_ptr(), T * C, C, w.data_ptr(), bias, C, K, ld.data_ptr(), B, T,
+                                       want_w.data_ptr(), want_p.data_ptr(), T, _hip.BF16, s), "conv_post")
+    got_w = torch.full((B, T), 7.0, device="cuda")
+    got_p = torch.full((B, T), 123, dtype=torch.int16, device="cuda")
+    _hip.check(lib.itts_act_conv_post_tanh(x.data_ptr(), T * C, C, up.data_ptr(), down.data_ptr(), la.data_ptr(),
+                                           lb.data_ptr(), w.data_ptr(), bias, C, K, ld.data_ptr(), B, T,
+                                           got_w.data_ptr(), got_p.data_ptr(), T, s), "fused tail")
     torch.cuda.synchronize()
-    for b, L in enumerate(lens):
-        gb, wb = got[b, :L].view(torch.int16).cpu(), want[b, :L].view(torch.int16).cpu()
-        bad = (gb != wb).nonzero()
-        assert bad.numel() == 0, (b, L, bad[:8].tolist())
+    gw, ww = got_w.cpu(), want_w.cpu()
+    bad = (gw.view(torch.int32) != ww.view(torch.int32)).nonzero()
+    assert bad.numel() == 0, (bad[:8].tolist(), lens.tolist())
+    assert torch.equal(got_p.cpu(), want_p.cpu())
+    assert bool((gw[:, :] == 7.0).logical_or(torch.arange(T)[None] < lens[:, None]).all())  # nothing past len

@@ -79,3 +79,52 @@ def test_beam_sample_first_token_distribution(beam_golden):
             counts[t] = counts.get(t, 0) + 1
     assert len(counts) <= 3  # only the top-3 tokens survive the warper
     assert max(counts.values()) > 100  # the most likely token wins most often
+
+
+def test_oracle_test_conveniences_keep_semantics(beam_golden):
+    """``copies`` / ``trace`` of generate_beam and the split prefill / decode weights (``sd_decode``) are
+    test conveniences: copies decode like the utterance repeated, the trace's last entry is the returned
+    state, and ``sd_decode`` = the same weights changes nothing (tiny config, CPU)."""
+    bg = beam_golden
+    o = oracle("tiny", 0.0, bg)
+    conds, text, n = torch.from_numpy(bg["tiny_conds"]), torch.from_numpy(bg["tiny_text"]), 12
+    with torch.no_grad():
+        one = o.generate_beam(conds, text, n)
+        tr = []
+        rep = o.generate_beam(conds, text, n, copies=3, trace=tr)
+        assert torch.equal(rep, one.expand(3, -1))
+        assert len(tr) == n and len(tr[-1]["seqs"]) == 9 and tr[-1]["vals"].shape == (3, 6)
+        assert all(len(q) == n for q in tr[-1]["seqs"])
+        o2 = GPTOracle({k: v.clone() for k, v in o.sd.items()}, tiny_config().gpt, sd_decode=o.sd)
+        assert torch.equal(o2.generate_beam(conds, text, n), one)
+        assert torch.equal(o2.generate(conds, text, n), o.generate(conds, text, n))
+        codes = o.generate(conds, text, n)
+        np.testing.assert_allclose(o2.forced_logits(conds, text, codes).numpy(),
+                                   o.forced_logits(conds, text, codes).numpy(), rtol=0, atol=2e-4)
+
+
+def test_bf16_effective_fold_is_exact_without_rounding():
+    """tests/parity_util.bf16_effective_gpt_sds (the bf16 product path's weight forms for the oracle): with the
+    rounding off, folding ln_1 / ln_2 into c_attn / c_fc is the same function (logits within f32 noise), and
+    with it on the logits move by a small amount (the weight rounding the GPU leg isolates)."""
+    from parity_util import bf16_effective_gpt_sds
+    cfg = tiny_config()
+    sd = {k: torch.from_numpy(np.asarray(v)).clone() for k, v in gpt_state_dict(cfg.gpt, 3, 0.15).items()}
+    g = torch.Generator().manual_seed(1)
+    for i in range(int(cfg.gpt.layers)):  # non-trivial LayerNorm affines
+        for ln in ("ln_1", "ln_2"):
+            sd[f"gpt.h.{i}.{ln}.weight"] = 1 + 0.2 * torch.randn(sd[f"gpt.h.{i}.{ln}.weight"].shape, generator=g)
+            sd[f"gpt.h.{i}.{ln}.bias"] = 0.1 * torch.randn(sd[f"gpt.h.{i}.{ln}.bias"].shape, generator=g)
+    conds = torch.randn(1, 32, int(cfg.gpt.model_dim), generator=g)
+    text = torch.randint(2, 200, (1, 10), generator=g)
+    base = GPTOracle(sd, cfg.gpt)
+    with torch.no_grad():
+        codes = base.generate(conds, text, 16, min_new_tokens=16)
+        want = base.forced_logits(conds, text, codes)
+        pre, dec = bf16_effective_gpt_sds(sd, int(cfg.gpt.layers), rounding=False)
+        exact = GPTOracle(pre, cfg.gpt, sd_decode=dec).forced_logits(conds, text, codes)
+        pre, dec = bf16_effective_gpt_sds(sd, int(cfg.gpt.layers))
+        rounded = GPTOracle(pre, cfg.gpt, sd_decode=dec).forced_logits(conds, text, codes)
+    assert float((exact - want).abs().max()) < 1e-4
+    d = float((rounded - want).abs().max())
+    assert 1e-4 < d < 0.2, d
