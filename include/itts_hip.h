@@ -387,6 +387,7 @@ typedef struct ItTsGptDecodeState {
   uint8_t* done;           /* [rows] */
   int32_t* codes;          /* [rows][max_new] */
   const int32_t* forced;   /* teacher forcing (tests) or NULL */
+  int num_beams;           /* beams per utterance of a kv_rows state (rows b * num_beams + k), else 0 (ABI 5) */
 } ItTsGptDecodeState;
 
 /* Token selection of the step: mode 0 greedy (itts_sample_embed), 1 top-k / top-p sampling

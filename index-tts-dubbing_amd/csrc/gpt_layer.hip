@@ -224,9 +224,15 @@ __device__ bool poll_ge(const uint32_t* ctr, uint32_t target, uint32_t* err, uin
 
 // H16 (steps of at most 16 rows, MT = 1): the c_attn / c_fc phases load and multiply only the first 16-row
 // half of their A operands (rows 16-31 are padding: their outputs, never read, come out as the fold terms)
-template <int MT, bool ROWS, int KB = kKB, bool H16 = false>
+// NBM (beam states of NBM beams, R <= 32 NBM): the attention runs ONE pass, unit (jj, u) taking utterance 2 jj + u
+// with all its beams (rows NBM ui + k): a key's lineage rows of the NBM beams are requested together (default cache
+// policy: where the beams share a row, one request fetches it and the others hit in L1 / L2), instead of MT passes
+// of one row per unit one after the other.  Per row the same arithmetic in the same order: bit-identical.
+template <int MT, bool ROWS, int KB = kKB, bool H16 = false, int NBM = 0>
 __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   static_assert(!H16 || MT == 1, "16-row halves: one row tile");
+  static_assert(NBM == 0 || (ROWS && !H16 && NBM >= 2 && NBM <= 4 && MT <= NBM), "beam-major: beam states");
+  constexpr int NLD = NBM > 0 ? NBM : 1;
   constexpr int WAUX = 2;              // LDS-DMA cache policy of the weight stream: non-temporal
   constexpr int NHF = H16 ? 1 : 2;     // 16-row halves of the A operands loaded / multiplied
   __shared__ __attribute__((aligned(16))) unsigned char lds_wo[8 * 1024];
@@ -289,6 +295,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   const int tu = tid - 256 * u, g = tu >> 3, d8 = tu & 7;
   constexpr int NG = 32;
   u32x4_t kr[KB], vr[KB];
+  u32x4_t kb[NLD][KB], vb[NLD][KB];  // NBM: every beam's rows of a round
   // K/V rows of key index jk (0-based from the row's first valid key) of row `row`: the row's own cache
   // row, or (beams) the row of kv_rows[row][position] that holds that prefix position
   auto kv_ptr = [&](const uint16_t* cache, int row, int pos, int jk) -> const uint16_t* {
@@ -310,6 +317,37 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     }
   };
   auto unit_row = [&](int pt) { return 32 * pt + 2 * jj + u; };
+  // NBM: this unit's utterance (NBM rows) and whether it exists
+  const int ui = 2 * jj + u;
+  const bool act_bm = NBM > 0 && NBM * ui < R;
+  const int uib = act_bm ? ui : 0;
+  // NBM: the lineage cache rows of the unit's beams (keys 0 .. nk-1) packed one byte a beam (rows < 128) into
+  // LDS; every thread of the workgroup calls it (it ends with the barrier the readers need)
+  auto stage_kvi_bm = [&](int p0, int nk) __attribute__((always_inline)) {
+    if constexpr (NBM > 0) {
+      const int32_t* src = p.kv_rows + (int64_t)(NBM * uib) * p.ld_rows + p0;
+      for (int i = tu; i < nk; i += 256) {
+        uint32_t pk = 0;
+#pragma unroll
+        for (int k = 0; k < NBM; ++k) pk |= (uint32_t)src[(int64_t)k * p.ld_rows + i] << (8 * k);
+        lds_kvi[u * kKviMax + i] = (int32_t)pk;
+      }
+      bar();
+    }
+  };
+  auto kv_load_bm = [&](u32x4_t (&dst)[NLD][KB], const uint16_t* cache, int p0, int nk, int j0) {
+#pragma unroll
+    for (int uu = 0; uu < KB; ++uu) {
+      const int jk = min(j0 + NG * uu + g, max(nk - 2, 0));
+      const uint32_t pk = (uint32_t)lds_kvi[u * kKviMax + jk];
+#pragma unroll
+      for (int k = 0; k < NLD; ++k) {
+        const int crow = (pk >> (8 * k)) & 255;
+        dst[k][uu] = *reinterpret_cast<const u32x4_t*>(cache + (int64_t)crow * p.cache_bs + (int64_t)h * p.cache_hs +
+                                                       (int64_t)(p0 + jk) * kHD + 8 * d8);
+      }
+    }
+  };
   // beams: this unit's lineage indices of row `row` (keys 0 .. nk-1) into LDS; every thread of the workgroup
   // calls it (it ends with the barrier the readers need)
   auto stage_kvi = [&](int row, int p0, int nk) __attribute__((always_inline)) {
@@ -366,11 +404,18 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   };
   // the attention's first round of K/V rows (pass 0)
   auto kv_round0 = [&]() {
-    const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
-    const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
-    stage_kvi(rr, p0, nk);
-    kv_load(kr, p.kc, rr, p0, nk, 0);
-    kv_load(vr, p.vc, rr, p0, nk, 0);
+    if constexpr (NBM > 0) {
+      const int p0 = p.pad ? p.pad[NBM * uib] : 0, nk = kidx + 1 - p0;
+      stage_kvi_bm(p0, nk);
+      kv_load_bm(kb, p.kc, p0, nk, 0);
+      kv_load_bm(vb, p.vc, p0, nk, 0);
+    } else {
+      const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
+      const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+      stage_kvi(rr, p0, nk);
+      kv_load(kr, p.kc, rr, p0, nk, 0);
+      kv_load(vr, p.vc, rr, p0, nk, 0);
+    }
   };
   // x^ rows of the NEXT row tiles were written by the previous launch: plain buffer loads (sc1, as any hand-off)
   const auto rsrc_xh = __builtin_amdgcn_make_buffer_rsrc(p.xh, 0, 0x7fffffff, 0x00020000);
@@ -530,6 +575,48 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   constexpr int NQ = 4, GPQ = 8;
   float* qsum = pv + 32 * kPvPitch;
   float* lsum = qsum + NQ * kPvPitch;
+  // the unit's 32 group partials (pv, gm, gl: written by the caller) -> o row r_store (fixed-order merge); every
+  // thread of the workgroup calls it
+  auto merge_store = [&](bool act, int r_store) __attribute__((always_inline)) {
+    bar();
+    if (act) {
+      const int dd = tu & (kHD - 1), qd = tu / kHD;
+      float M = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
+      float Ls = 0.f, a = 0.f;
+#pragma unroll
+      for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
+        const float wgt = __expf(gm[i] - M);
+        Ls = fmaf(gl[i], wgt, Ls);
+        a = fmaf(pv[i * kPvPitch + dd], wgt, a);
+      }
+      qsum[qd * kPvPitch + dd] = a;
+      if (dd == 0) lsum[qd] = Ls;
+    }
+    bar();
+    if (tu < kHD) {
+      float v = 0.f;
+      if (act) {
+        float Ls = 0.f, a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+          Ls += lsum[i];
+          a += qsum[i * kPvPitch + tu];
+        }
+        v = a / Ls;
+      }
+      obf[u * kHD + tu] = f2bf(v);
+    }
+    bar();
+    if (tu < 8) {  // o rows -> the cluster's [rows][128] tile, write-through 16-B stores
+      const int d0 = 8 * tu;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(kOffOb), ((c * kMaxR + r_store) * 128 + hh * kHD + d0) * 2, 0,
+                                             PL_AUX);
+    }
+  };
+  if constexpr (NBM == 0) {
 #pragma unroll 1
   for (int pt = 0; pt < MT; ++pt) {
     const int r_u = unit_row(pt);
@@ -659,44 +746,139 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
         gl[g] = l_run;
       }
     }
-    bar();
-    if (act_u) {
-      const int dd = tu & (kHD - 1), qd = tu / kHD;
-      float M = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < NG; ++i) M = fmaxf(M, gm[i]);
-      float Ls = 0.f, a = 0.f;
-#pragma unroll
-      for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
-        const float wgt = __expf(gm[i] - M);
-        Ls = fmaf(gl[i], wgt, Ls);
-        a = fmaf(pv[i * kPvPitch + dd], wgt, a);
-      }
-      qsum[qd * kPvPitch + dd] = a;
-      if (dd == 0) lsum[qd] = Ls;
-    }
-    bar();
-    if (tu < kHD) {
-      float v = 0.f;
-      if (act_u) {
-        float Ls = 0.f, a = 0.f;
-#pragma unroll
-        for (int i = 0; i < NQ; ++i) {
-          Ls += lsum[i];
-          a += qsum[i * kPvPitch + tu];
-        }
-        v = a / Ls;
-      }
-      obf[u * kHD + tu] = f2bf(v);
-    }
-    bar();
-    if (tu < 8) {  // o rows -> the cluster's [rows][128] tile, write-through 16-B stores
-      const int d0 = 8 * tu;
-      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obf + u * kHD + d0);
-      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(kOffOb), ((c * kMaxR + r_u) * 128 + hh * kHD + d0) * 2, 0, PL_AUX);
-    }
+    merge_store(act_u, r_u);
     if (MT > 1) bar();  // the unit scratch and obf are reused by the next pass
   }
+  } else {
+  // ---- NBM: ONE pass over the unit's utterance, all its beams per key round ----
+  float* bq = pv;  // [NBM][q | k | v][64] of this step (the merge scratch is free until the key loop ends)
+  {
+    const int p0 = p.pad ? p.pad[NBM * uib] : 0, nk = kidx + 1 - p0;
+    if ((w & 3) < NBM && act_bm) {  // wave k of the unit sweeps beam k's 192 granules
+      const int kk = w & 3, r_k = NBM * ui + kk;
+      const uint64_t* src = gq + ((int64_t)r_k * kH + h) * 192;
+      uint64_t g0, g1, g2;
+      bool ok = false;
+      for (uint32_t n = 0; !dead; ++n) {
+        g0 = ld_sc1_u64(src + lane);
+        g1 = ld_sc1_u64(src + 64 + lane);
+        g2 = ld_sc1_u64(src + 128 + lane);
+        const bool mine = (uint32_t)(g0 >> 32) == L1 && (uint32_t)(g1 >> 32) == L1 && (uint32_t)(g2 >> 32) == L1;
+        if (__all(mine)) {
+          ok = true;
+          break;
+        }
+        if (n > kSpinMax || ((n & 255) == 255 && ld_relaxed(err) != 0)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!ok) {
+        if (lane == 0) {
+          if (!dead) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, PL_SCOPE);
+          *abort_flag = 1;
+        }
+      } else {
+        bq[kk * 192 + lane] = (0.f + __uint_as_float((uint32_t)g0)) * 0.125f;  // 1/sqrt(64), exact
+        bq[kk * 192 + 64 + lane] = 0.f + __uint_as_float((uint32_t)g1);
+        bq[kk * 192 + 128 + lane] = 0.f + __uint_as_float((uint32_t)g2);
+      }
+    }
+    bar();
+    mark(3);
+    if (*abort_flag || dead) return;
+    issue_dma();
+    float o8[NLD][8], m_run[NLD], l_run[NLD], q[NLD][8];
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      m_run[k] = -INFINITY;
+      l_run[k] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o8[k][e] = 0.f;
+        q[k][e] = bq[k * 192 + 8 * d8 + e];
+      }
+    }
+    if (act_bm) {
+      auto unpack = [&](const u32x4_t& r, float (&xv)[8]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          xv[2 * i] = __uint_as_float(r[i] << 16);
+          xv[2 * i + 1] = __uint_as_float(r[i] & 0xFFFF0000u);
+        }
+      };
+      // one round of KB keys per group for every beam: the per-row arithmetic of key_round (same chunks, same
+      // order); this step's own key / value (keys >= nk - 1) from the granules in LDS
+      auto key_round_bm = [&](int j0) __attribute__((always_inline)) {
+        float sc[NLD][KB];
+#pragma unroll
+        for (int k = 0; k < NLD; ++k)
+#pragma unroll
+          for (int uu = 0; uu < KB; ++uu) {
+            const int jk = j0 + NG * uu + g;
+            float kx[8];
+            unpack(kb[k][uu], kx);
+            if (jk >= nk - 1) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) kx[e] = bq[k * 192 + 64 + 8 * d8 + e];
+            }
+            float pt_ = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) pt_ = fmaf(q[k][e], kx[e], pt_);
+            pt_ = sum8_dpp(pt_);
+            sc[k][uu] = jk < nk ? pt_ : -INFINITY;
+          }
+        kv_load_bm(kb, p.kc, p0, nk, j0 + NG * KB);
+#pragma unroll
+        for (int k = 0; k < NLD; ++k)
+#pragma unroll
+          for (int c0 = 0; c0 < KB; c0 += kSub) {
+            float bm = -INFINITY;
+#pragma unroll
+            for (int uu = c0; uu < c0 + kSub; ++uu) bm = fmaxf(bm, sc[k][uu]);
+            if (bm == -INFINITY) continue;
+            const float mn = fmaxf(m_run[k], bm);
+            const float corr = __expf(m_run[k] - mn);
+            l_run[k] *= corr;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o8[k][e] *= corr;
+#pragma unroll
+            for (int uu = c0; uu < c0 + kSub; ++uu) {
+              const int jk = j0 + NG * uu + g;
+              const float pr = __expf(sc[k][uu] - mn);
+              l_run[k] += pr;
+              float vx[8];
+              unpack(vb[k][uu], vx);
+              if (jk >= nk - 1) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) vx[e] = bq[k * 192 + 128 + 8 * d8 + e];
+              }
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o8[k][e] = fmaf(pr, vx[e], o8[k][e]);
+            }
+            m_run[k] = mn;
+          }
+        kv_load_bm(vb, p.vc, p0, nk, j0 + NG * KB);
+      };
+      key_round_bm(0);
+      mark(21);
+      for (int j0 = NG * KB; j0 < nk; j0 += NG * KB) key_round_bm(j0);
+      mark(20);
+    }
+    // beam by beam: partials -> merge -> o row (the unit scratch, bq included, is free now)
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      bar();  // (k = 0: every wave is past its reads of bq)
+      if (act_bm) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[k][e];
+        if (d8 == 0) {
+          gm[g] = m_run[k];
+          gl[g] = l_run[k];
+        }
+      }
+      merge_store(act_bm, NBM * ui + k);  // (a unit past the utterances writes zeros to rows >= R, as a pass does)
+    }
+  }
+  }  // NBM
   mark(4);
   drain();  // the o stores, and this wave's weight DMA (read from LDS from phase C on)
   bar();
@@ -967,9 +1149,18 @@ int occ_ok(int slot) {
   if (g_occ[slot] < 0) {
     switch (slot) {
       case 0: g_occ[0] = fits(gpt_layer_pl_kernel<1, false, kKBSmall, kSmallH16>); break;
-      case 1: g_occ[1] = fits(gpt_layer_pl_kernel<1, false>) & fits(gpt_layer_pl_kernel<1, true>); break;
-      case 2: g_occ[2] = fits(gpt_layer_pl_kernel<2, false>) & fits(gpt_layer_pl_kernel<2, true>); break;
-      case 3: g_occ[3] = fits(gpt_layer_pl_kernel<3, false>) & fits(gpt_layer_pl_kernel<3, true>); break;
+      case 1:
+        g_occ[1] = fits(gpt_layer_pl_kernel<1, false>) & fits(gpt_layer_pl_kernel<1, true>) &
+                   fits(gpt_layer_pl_kernel<1, true, kKB, false, 3>);
+        break;
+      case 2:
+        g_occ[2] = fits(gpt_layer_pl_kernel<2, false>) & fits(gpt_layer_pl_kernel<2, true>) &
+                   fits(gpt_layer_pl_kernel<2, true, kKB, false, 3>);
+        break;
+      case 3:
+        g_occ[3] = fits(gpt_layer_pl_kernel<3, false>) & fits(gpt_layer_pl_kernel<3, true>) &
+                   fits(gpt_layer_pl_kernel<3, true, kKB, false, 3>);
+        break;
       default: g_occ[4] = fits(gpt_layer_pl_kernel<4, false>) & fits(gpt_layer_pl_kernel<4, true>); break;
     }
   }
@@ -1030,6 +1221,16 @@ bool layer_ok(const ItTsGptLayerW* ly, const ItTsGptPlLayerW* pl) {
          ly->proj_b && ly->o_c;
 }
 
+// beam states of num_beams = 3 and at most 96 rows run the beam-major attention (ITTS_PL_BEAM_SHARED=0: the
+// row passes, bit-identical; A/B)
+bool beam_major(const ItTsGptDecodeState* st) {
+  static const bool on = [] {
+    const char* e = getenv("ITTS_PL_BEAM_SHARED");
+    return !(e && e[0] == '0');
+  }();
+  return on && st->kv_rows && st->num_beams == 3 && st->rows % 3 == 0 && st->rows <= 96;
+}
+
 // layer `layer` of decode step kstep as ONE launch
 int launch_layer(const ItTsGptLayerW* lyw, const ItTsGptPlLayerW* plw, const ItTsGptDecodeState* st, int layer,
                  int kstep, int last, void* scratch, hipStream_t s, const char* fn) {
@@ -1056,6 +1257,14 @@ int launch_layer(const ItTsGptLayerW* lyw, const ItTsGptPlLayerW* plw, const ItT
   a.scratch = static_cast<unsigned char*>(scratch);
   const int mt = (st->rows + 31) / 32;
   const int ki = 2 * (mt - 1) + (st->kv_rows ? 1 : 0);
+  if (beam_major(st)) {  // beam3 states of <= 96 rows: one attention pass over each utterance's beams
+    switch (mt) {
+      case 1: hipLaunchKernelGGL((gpt_layer_pl_kernel<1, true, kKB, false, 3>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((gpt_layer_pl_kernel<2, true, kKB, false, 3>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+      default: hipLaunchKernelGGL((gpt_layer_pl_kernel<3, true, kKB, false, 3>), dim3(kWG), dim3(kThreads), 0, s, a); break;
+    }
+    return itts::check_launch(fn);
+  }
   if (ki == 0 && st->rows <= kSmallRows) {  // kSmallRows <= 16: one 16-row half
     hipLaunchKernelGGL((gpt_layer_pl_kernel<1, false, kKBSmall, kSmallH16>), dim3(kWG), dim3(kThreads), 0, s, a);
     return itts::check_launch(fn);

@@ -25,8 +25,9 @@ int check_launch(const char* fn) {
 
 extern "C" const char* itts_last_error(void) { return itts::g_last_error.c_str(); }
 
-extern "C" int itts_abi_version(void) { return 4; }  // 3: persistent decode layer, attn.c_proj split-K;
-                                                     // 4: epoch-tagged hand-offs (itts_gpt_pl_reset), host packers
+extern "C" int itts_abi_version(void) { return 5; }  // 3: persistent decode layer, attn.c_proj split-K;
+                                                     // 4: epoch-tagged hand-offs (itts_gpt_pl_reset), host packers;
+                                                     // 5: ItTsGptDecodeState.num_beams, itts_act_conv_post_tanh
 
 // Which gfx target this code object was built for (sanity check from the host).
 extern "C" const char* itts_build_target(void) { return "gfx950"; }

@@ -131,7 +131,7 @@ class GptDecodeState(ctypes.Structure):
     _fields_ = [("rows", _c_i), ("max_kv", _c_i), ("kv_base", _c_i), ("max_new", _c_i)] + \
         [(n, _vp) for n in ("x", "xh", "qkv", "o", "f", "part", "logits", "k_cache", "v_cache", "pad", "tstate",
                             "kv_rows")] + \
-        [("ld_rows", _c_i64)] + [(n, _vp) for n in ("seen", "done", "codes", "forced")]
+        [("ld_rows", _c_i64)] + [(n, _vp) for n in ("seen", "done", "codes", "forced")] + [("num_beams", _c_i)]
 
 
 class GptSeqLayerW(ctypes.Structure):

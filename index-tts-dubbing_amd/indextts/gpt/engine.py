@@ -492,7 +492,7 @@ class HipGPT:
             st["B"], self.max_kv, st["s"] + 1, st["max_new"], p(st["x"]), p(st["h"]), p(st["qkv"]), p(st["o"]),
             p(st["f"]), p(st["ws"]), p(st["logits"]), p(st["kc"]), p(st["vc"]), p(st["pad"]), p(st["t"]), p(kv_rows),
             0 if kv_rows is None else kv_rows.stride(0), p(st["seen"]), p(st["done"]), p(st["codes"]),
-            p(st.get("forced")))
+            p(st.get("forced")), int(st["beam"]["K"]) if kv_rows is not None and "beam" in st else 0)
 
     def _decode_step_c(self, st, min_new, penalty, nsteps=1):
         """bf16 product decode step as ONE C-ABI call (itts_gpt_decode_step, gpt_step.hip): the launches

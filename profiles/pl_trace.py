@@ -25,9 +25,13 @@ def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
     conds = torch.randn(B, 32, 1024, generator=g).cuda()
     for k in list(eng._lanes):
         del eng._lanes[k]
-    eng.generate(conds, text, steps, min_new_tokens=steps)
+    nb = int(os.environ.get("BEAMS", "1"))  # BEAMS=3: B / 3 utterances, beam search (B rows)
+    if nb > 1:
+        eng.generate(conds[: B // nb], text[: B // nb], steps, min_new_tokens=steps, num_beams=nb)
+    else:
+        eng.generate(conds, text, steps, min_new_tokens=steps)
     torch.cuda.synchronize()
-    OFF_TRACE = int(eng.lib.itts_gpt_pl_scratch_bytes()) - 512 - 256 * 32 * 8  # trace, epoch, error blocks
+    OFF_TRACE = int(eng.lib.itts_gpt_pl_scratch_bytes()) - 256 - 256 * 32 * 8  # trace, then the epoch / error block
     tr = eng._pl_scratch.view(torch.uint8)[OFF_TRACE:OFF_TRACE + 256 * 32 * 8].view(torch.int64).view(256, 32)
     tr = tr[:, :22].cpu().double()
     t0 = tr[:, 0].min()

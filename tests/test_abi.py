@@ -51,7 +51,7 @@ def test_ctypes_table_matches_header():
 
 
 def test_runtime_queries(lib):
-    assert lib.itts_abi_version() == 4
+    assert lib.itts_abi_version() == 5
     assert lib.itts_build_target() == b"gfx950"
 
 

@@ -99,15 +99,20 @@ def test_persistent_layer_free_running_equals_chain():
 
 
 @pytest.mark.parametrize("do_sample", [False, True])
-def test_persistent_layer_beams_equal_chain(do_sample):
-    """beam search / beam sample (3 beams x 32 utterances = 96 rows, keys through the lineage table) on the
-    persistent layers: the same hypotheses as on the launch chain"""
+@pytest.mark.parametrize("nutt", [32, 10, 21])
+def test_persistent_layer_beams_equal_chain(do_sample, nutt):
+    """beam search / beam sample (3 beams x 32 / 10 / 21 utterances = 96 / 30 / 63 rows: one to three row tiles,
+    keys through the lineage table; the beam-major attention, one pass over each utterance's beams) on the
+    persistent layers: the same hypotheses as on the launch chain; ragged text lengths (left padding) for 10 / 21"""
     eng = _engine()
-    if not eng.pl or not eng._pl_ok({"B": 96}):
+    if not eng.pl or not eng._pl_ok({"B": 3 * nutt, "kv_rows": True}):
         pytest.skip("persistent layer not available on this device")
-    g = torch.Generator().manual_seed(91)
-    text = torch.randint(2, 12000, (32, 30), generator=g).cuda()
-    conds = torch.randn(32, 32, 1024, generator=g).cuda()
+    g = torch.Generator().manual_seed(91 + nutt)
+    L = 30
+    lens = [L] * nutt if nutt == 32 else [int(torch.randint(5, L + 1, (1,), generator=g)) for _ in range(nutt)]
+    text = torch.stack([torch.nn.functional.pad(torch.randint(2, 12000, (n,), generator=g), (0, L - n), value=1)
+                        for n in lens]).cuda()
+    conds = torch.randn(nutt, 32, 1024, generator=g).cuda()
     outs = []
     for pl in (True, False):
         eng.pl = pl
