@@ -44,7 +44,7 @@ def load(d, counter):
 def short(name):
     for k in sorted(DECODE_KERNELS, key=len, reverse=True) + ["igemm256_kernel", "igemm_kernel", "amp_conv_kernel",
                                                               "aa_snakebeta_kernel",
-                                                              "aa_snake_mfma_kernel"]:
+                                                              "aa_snake_mfma_kernel", "act_post_conv_kernel"]:
         if k in name:
             return k
     return name.split("(")[0][-40:]
@@ -55,7 +55,9 @@ def vocoder(fetch, write):
     groups = {"igemm_kernel": lambda n: "igemm_kernel" in n or "igemm256_kernel" in n,  # both tile families
               "amp_conv_kernel": lambda n: "amp_conv_kernel" in n,  # conv-only and act-fused forms
               # the activation: MFMA kernel on the vocoder's bf16 channel-last layout (VALU kernel otherwise)
-              "aa_snakebeta_kernel": lambda n: "aa_snakebeta_kernel" in n or "aa_snake_mfma_kernel" in n}
+              "aa_snakebeta_kernel": lambda n: "aa_snakebeta_kernel" in n or "aa_snake_mfma_kernel" in n,
+              # round 6: activation_post + conv_post + tanh + int16 in one launch
+              "act_post_conv_kernel": lambda n: "act_post_conv_kernel" in n}
     for name, match in groups.items():
         ids = sorted(k for k, (n, _) in fetch.items() if match(n) and k in write)
         ids = ids[len(ids) // 2:]
@@ -68,6 +70,7 @@ def vocoder(fetch, write):
     out["igemm_bytes_per_launch"] = out.get("igemm_kernel", {}).get("bytes_per_launch")
     out["amp_conv_bytes_per_launch"] = out.get("amp_conv_kernel", {}).get("bytes_per_launch")
     out["aa_snakebeta_bytes_per_launch"] = out.get("aa_snakebeta_kernel", {}).get("bytes_per_launch")
+    out["act_post_conv_bytes_per_launch"] = out.get("act_post_conv_kernel", {}).get("bytes_per_launch")
     out["correction"] = "FETCH_SIZE x2 (gfx950 coalesced-read undercount); KiB -> bytes"
     return out
 
