@@ -24,7 +24,8 @@
 //   E2 o -> attn.c_proj: write-through stores, drain, one counter per cluster (32 adders).
 //   C  attn.c_proj split c: 32 output columns (tile j), 8 k-steps of 16 (one per wave) -> partial.
 //   E3 partials -> reduce: one counter per column tile j (8 adders, one per cluster).
-//   D  x1 = x + (b_o + sum_c partial_c) for tile j, x1^ -> the cluster's copy of x^ (E4: 32 adders).
+//   D  tile j's owner (cluster j % 8, round 6): x1 = x + (b_o + sum_c partial_c), x1^ -> every cluster's copy (E4:
+//      32 adders, the tile owners) and f32 x1 for phase G; the other workgroups go straight to E4.
 //   E  c_fc (ln_2 folded) + gelu: 16 columns (tile 32c + j), A = the cluster's x1^.
 //   E5 f -> mlp.c_proj: cluster counter (32 adders).
 //   F  mlp.c_proj split c: 32 columns (tile j), 32 k-steps of 16 (4 per wave) -> partial.
@@ -123,7 +124,8 @@ constexpr int64_t kOffP1 = kOffOb + (int64_t)kNC * kMaxR * 128 * 2;   // [8][128
 constexpr int64_t kOffXc = kOffP1 + (int64_t)kNC * kMaxR * kD * 4;    // [8][128][1024] bf16
 constexpr int64_t kOffFc = kOffXc + (int64_t)kNC * kMaxR * kD * 2;    // [8][128][512] bf16
 constexpr int64_t kOffP2 = kOffFc + (int64_t)kNC * kMaxR * 512 * 2;   // [8][128][1024] f32
-constexpr int64_t kOffTrace = kOffP2 + (int64_t)kNC * kMaxR * kD * 4;  // [256 WG][32] u64 (ITTS_PL_TRACE builds)
+constexpr int64_t kOffX1 = kOffP2 + (int64_t)kNC * kMaxR * kD * 4;    // [128][1024] f32: x1 (phase D -> phase G)
+constexpr int64_t kOffTrace = kOffX1 + (int64_t)kMaxR * kD * 4;       // [256 WG][32] u64 (ITTS_PL_TRACE builds)
 constexpr int64_t kOffSeq = kOffTrace + (int64_t)kWG * 32 * 8;        // u32 epoch: launches since the reset
 constexpr int64_t kOffErr = kOffSeq + 4;  // sticky error word, beside the epoch: one 8-B load reads both
 constexpr int64_t kScratchBytes = kOffSeq + 256;
@@ -863,19 +865,75 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       for (int j0 = NG * KB; j0 < nk; j0 += NG * KB) key_round_bm(j0);
       mark(20);
     }
-    // beam by beam: partials -> merge -> o row (the unit scratch, bq included, is free now)
+    // every beam's partials -> merge -> o row, the beams side by side (three barriers for all of them, not three
+    // per beam): beam 0 in the unit scratch, beams 1.. in areas of `red` and of the lineage table (both free now);
+    // the merge arithmetic and order are merge_store's
+    constexpr int kArea = kPvRows * kPvPitch + 2 * 32;  // floats: pv (+ the qsum / lsum rows), gm, gl
+    static_assert(NBM == 0 || 2 * (NBM - 1) * kArea <= 8192 + (ROWS ? 2 * kKviMax : 0), "merge areas fit");
+    auto area = [&](int k) -> float* {  // beam k >= 1 of this unit: red first, then the lineage table
+      const int a = 2 * (k - 1) + u;
+      return a * kArea + kArea <= 8192 ? red + a * kArea
+                                       : reinterpret_cast<float*>(lds_kvi) + (a * kArea - (8192 / kArea) * kArea);
+    };
+    bar();  // every wave is past its reads of bq and of the lineage table
+    if (act_bm) {
 #pragma unroll
-    for (int k = 0; k < NLD; ++k) {
-      bar();  // (k = 0: every wave is past its reads of bq)
-      if (act_bm) {
+      for (int k = 0; k < NLD; ++k) {
+        float* pk = k == 0 ? pv : area(k);
+        float* gk = k == 0 ? gm : pk + kPvRows * kPvPitch;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) pv[g * kPvPitch + 8 * d8 + e] = o8[k][e];
+        for (int e = 0; e < 8; ++e) pk[g * kPvPitch + 8 * d8 + e] = o8[k][e];
         if (d8 == 0) {
-          gm[g] = m_run[k];
-          gl[g] = l_run[k];
+          gk[g] = m_run[k];
+          gk[32 + g] = l_run[k];
         }
       }
-      merge_store(act_bm, NBM * ui + k);  // (a unit past the utterances writes zeros to rows >= R, as a pass does)
+    }
+    bar();
+    if (act_bm) {
+      const int dd = tu & (kHD - 1), qd = tu / kHD;
+#pragma unroll
+      for (int k = 0; k < NLD; ++k) {
+        float* pk = k == 0 ? pv : area(k);
+        const float* gk = k == 0 ? gm : pk + kPvRows * kPvPitch;
+        const float* lk = k == 0 ? gl : gk + 32;
+        float M = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < NG; ++i) M = fmaxf(M, gk[i]);
+        float Ls = 0.f, a = 0.f;
+#pragma unroll
+        for (int i = qd * GPQ; i < qd * GPQ + GPQ; ++i) {
+          const float wgt = __expf(gk[i] - M);
+          Ls = fmaf(lk[i], wgt, Ls);
+          a = fmaf(pk[i * kPvPitch + dd], wgt, a);
+        }
+        pk[(32 + qd) * kPvPitch + dd] = a;  // qsum rows
+        if (dd == 0) pk[36 * kPvPitch + qd] = Ls;  // lsum row
+      }
+    }
+    bar();
+    uint16_t* obm = reinterpret_cast<uint16_t*>(smem + L_OBF);  // [2 units][NLD][64] bf16 (fits the 1-KB o / f stage)
+    if (tu < NLD * kHD) {
+      const int k = tu / kHD, d = tu & (kHD - 1);
+      float v = 0.f;
+      if (act_bm) {
+        const float* pk = k == 0 ? pv : area(k);
+        float Ls = 0.f, a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+          Ls += pk[36 * kPvPitch + i];
+          a += pk[(32 + i) * kPvPitch + d];
+        }
+        v = a / Ls;
+      }
+      obm[(u * NLD + k) * kHD + d] = f2bf(v);
+    }
+    bar();
+    if (tu < 8 * NLD) {  // o rows NBM ui + k -> the cluster's [rows][128] tile (a unit past the utterances: zeros)
+      const int k = tu >> 3, d0 = 8 * (tu & 7);
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(obm + (u * NLD + k) * kHD + d0);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(kOffOb), ((c * kMaxR + NBM * ui + k) * 128 + hh * kHD + d0) * 2,
+                                             0, PL_AUX);
     }
   }
   }  // NBM
@@ -933,14 +991,19 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   mark(16);
   if (tid == 0) add_relaxed(cnt_(CNT3 + j));
 
-  // ---- (D) x1 = x + (b_o + sum_c partial_c) on tile j (residual_reduce_ln_v4 order), x1^ -> cluster copy
-  if (tid == 0 && !poll_ge(cnt_(CNT3 + j), kNC * L1, err, 3)) *abort_flag = 1;
-  mark(7);
-  bar();
-  if (*abort_flag) return;
+  // ---- (D) x1 = x + (b_o + sum_c partial_c) on tile j (residual_reduce_ln_v4 order), by the tile's owner only
+  // (cluster j % 8): one reduce per tile instead of eight (the 8 partial slabs of a tile were read by all eight
+  // clusters: 8 MB per layer at 32 rows), x1^ stored into every cluster's copy (16-B write-through stores, 8 columns
+  // gathered over 4 lanes), f32 x1 into the x1 slab for the other clusters' phase G
+  const bool owner = c == (j & (kNC - 1));
   float2 x1[MT];
-  {
+  if (owner) {
+    if (tid == 0 && !poll_ge(cnt_(CNT3 + j), kNC * L1, err, 3)) *abort_flag = 1;
+    mark(7);
+    bar();
+    if (*abort_flag) return;
     const float2 ob2 = *reinterpret_cast<const float2*>(Ly.o_b + xcol);
+    const auto rxc = rsrc_of(kOffXc), rx1 = rsrc_of(kOffX1);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int row = 32 * t + xrow;
@@ -953,23 +1016,42 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       }
       const float2 xo = row < R ? x_raw[t] : float2{0.f, 0.f};
       x1[t] = float2{xo.x + pp.x, xo.y + pp.y};
-      st_sc1_u32(reinterpret_cast<uint32_t*>(xc + (((int64_t)c * kMaxR + row) * kD + xcol) * 2), pack2bf(x1[t].x, x1[t].y));
+      const uint32_t pk = pack2bf(x1[t].x, x1[t].y);
+      const uint32_t n1 = __shfl_down(pk, 1, 64), n2 = __shfl_down(pk, 2, 64), n3 = __shfl_down(pk, 3, 64);
+      if ((lane & 3) == 0) {
+#pragma unroll
+        for (int cc = 0; cc < kNC; ++cc)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{pk, n1, n2, n3}, rxc, ((cc * kMaxR + row) * kD + xcol) * 2, 0,
+                                                 PL_AUX);
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(x1[t].x), __float_as_uint(x1[t].y)}, rx1,
+                                            (row * kD + xcol) * 4, 0, PL_AUX);
     }
+    mark(8);
+    drain();
+    bar();
+    mark(17);
+    if (tid < kNC) add_relaxed(cnt_(CNT4 + tid));  // one wave instruction, one lane per cluster's counter
   }
-  mark(8);
-  drain();
-  bar();
-  mark(17);
-  if (tid == 0) add_relaxed(cnt_(CNT4 + c));
 
   // ---- (E) c_fc (ln_2 folded) + gelu on column tile 32c + j, per row tile, A = the cluster's x1^
   if (tid == 0 && !poll_ge(cnt_(CNT4 + c), kCPC * L1, err, 4)) *abort_flag = 1;
-  // past this poll every workgroup of the grid has added at E3 (cluster c's 32 E4 adders each waited for
-  // the 8 clusters of its tile), so all have read the epoch: workgroup 0 advances it for the next launch
+  // past this poll every workgroup of the grid has added at E3 (the 32 tile owners, whose adds this counter holds,
+  // each waited for the 8 clusters of its tile), so all have read the epoch: workgroup 0 advances it
   if (b == 0 && tid == 0 && !*abort_flag) st_sc1_u32(seq, L1);
   mark(9);
   bar();
   if (*abort_flag) return;
+  // phase G's x1 rows (wave c: rows 4c .. 4c+3 of every tile) of a tile this workgroup does not own: requested now,
+  // beside the c_fc operands (visible: every owner drained before its E4 add)
+  if (!owner && w == c) {
+    const auto rx1 = rsrc_of(kOffX1);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rx1, ((32 * t + xrow) * kD + xcol) * 4, 0, PL_AUX);
+      x1[t] = float2{__uint_as_float(v[0]), __uint_as_float(v[1])};
+    }
+  }
   {
     auto rsrc = rsrc_of(kOffXc);
     auto rsrc_f = rsrc_of(kOffFc);
