@@ -78,6 +78,12 @@ constexpr int kKBSmall = ITTS_PL_KB_SMALL, kSmallRows = ITTS_PL_SMALL_ROWS;
 #ifndef ITTS_PL_DMA_SPLIT  // small steps: an idle unit's waves issue the weight DMA of a half-active workgroup
 #define ITTS_PL_DMA_SPLIT 1
 #endif
+// full steps: only attn.c_proj's slice (8 KiB) goes out with the attention; the c_fc / mlp.c_proj slices (64 KiB)
+// after the E2 add, in the hand-off's idle window (the first key round waits for every DMA the wave issued before
+// it: the compiler's vmcnt(0) after an LDS-DMA)
+#ifndef ITTS_PL_DMA_TAIL
+#define ITTS_PL_DMA_TAIL 1
+#endif
 #ifndef ITTS_PL_SMALL_H16  // small steps also skip the second 16-row half of the c_attn / c_fc A operands
 #define ITTS_PL_SMALL_H16 1
 #endif
@@ -399,9 +405,17 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
         for (int m = 0; m < 18; ++m) dma_one(w - 4 + 4 * m);
       }
+    } else if (ITTS_PL_DMA_TAIL) {
+      dma_one(w);  // attn.c_proj's slice; the rest in issue_dma_tail
     } else {
 #pragma unroll
       for (int m = 0; m < 9; ++m) dma_one(w + 8 * m);
+    }
+  };
+  auto issue_dma_tail = [&]() {
+    if (ITTS_PL_DMA_TAIL && !dma_split) {
+#pragma unroll
+      for (int m = 1; m < 9; ++m) dma_one(w + 8 * m);
     }
   };
   // the attention's first round of K/V rows (pass 0)
@@ -942,6 +956,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   bar();
   mark(15);
   if (tid == 0) add_relaxed(cnt_(CNT2 + c));
+  issue_dma_tail();  // c_fc / mlp.c_proj slices (read from phase E on: drained at phase C's end)
 
   // ---- (C) attn.c_proj split c, tile j, per 32-row tile: decode_gemm_kernel EPI 2 (one k-step per wave)
   if (tid == 0 && !poll_ge(cnt_(CNT2 + c), kCPC * L1, err, 2)) *abort_flag = 1;
