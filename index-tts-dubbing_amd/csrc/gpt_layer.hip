@@ -412,7 +412,12 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       for (int m = 0; m < 9; ++m) dma_one(w + 8 * m);
     }
   };
-  auto issue_dma_tail = [&]() {
+  // the c_fc / mlp.c_proj slices (instructions 8 .. 71), every wave, after the E2 add (ITTS_PL_DMA_TAIL).
+  // Measured and not kept (profiles/dmatail_r06fg.txt, dmatail_r06hk.txt): the burst by waves 1-7 only (the E2
+  // poller none), the mlp.c_proj half after the E3 add, and the burst by the six waves that store no o row as their
+  // key loop ends or once the merge is past their last LDS read -- issuing 64 KiB of DMA holds a CU's memory pipe
+  // for ~2.5 us wherever it goes, and only the E2 wait has that much idle time
+  auto issue_dma_tail = [&]() __attribute__((always_inline)) {
     if (ITTS_PL_DMA_TAIL && !dma_split) {
 #pragma unroll
       for (int m = 1; m < 9; ++m) dma_one(w + 8 * m);
