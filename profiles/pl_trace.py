@@ -46,6 +46,9 @@ def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
         col = rel[:, i]
         ok = col.abs() < 1e6  # D's marks (7, 8, 17) are stamped by the tile owners only (round 6)
         cv = col[ok]
+        if cv.numel() == 0:  # a mark this build does not stamp
+            prev = None
+            continue
         line = f"  {i:2d} {n:14s} min {float(cv.min()):7.2f} med {float(cv.median()):7.2f} max {float(cv.max()):7.2f}"
         if int(ok.sum()) < 256:
             line += f" ({int(ok.sum())} WGs)"
@@ -68,6 +71,8 @@ def run(eng, B, L_text=48, steps=int(os.environ.get("STEPS", "40"))):
             add, rdy = add[add.abs() < 1e6], rdy[rdy.abs() < 1e6]
             if add.numel() and rdy.numel():
                 lat.append(rdy - add.max())
+        if not lat:
+            continue
         lat = torch.cat(lat)
         print(f"  {name}: last add -> ready  min {float(lat.min()):5.2f} med {float(lat.median()):5.2f} "
               f"max {float(lat.max()):5.2f} us", flush=True)
