@@ -12,7 +12,7 @@ Also reports ``roofline``: the dominant unit of work, the hipGraph-replayed GPT 
 the step; HBM-bound): algorithmic bytes (every weight byte + the K/V rows attended) per replay /
 the replay's duration from HIP events recorded on the decode stream around each replay, and
 ``traffic`` = measured HBM bytes per step from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the
-current build (profiles/run_profiles_r05.sh -> the TRAFFIC_DECODE file below); ``roofline_vocoder_conv``:
+current build (profiles/run_profiles_r06.sh -> the TRAFFIC_DECODE file below); ``roofline_vocoder_conv``:
 the MFMA implicit GEMM running the BigVGAN convs, and the HBM-bound vocoder kernels (activation, AMP
 convs, fused conv -> activation), from HIP events around each launch; and ``cpu_baseline``: the fp32
 oracle (a CPU restatement of the reference path) on a bounded sample, on this host's cores.
@@ -40,10 +40,10 @@ PEAK_HBM_GBS = 8000.0
 # per decoding and decode path (persistent layers or the launch chain): None until measured for this build
 # PMC files are measured on the C3 workload (profiles/pmc_decode.py, pmc_vocoder.py): other workloads report
 # traffic null rather than C3's bytes
-TRAFFIC_DECODE = {("c3", "greedy", True): "traffic_decode_pl_r05zh.json", ("c3", "greedy", False): "traffic_decode_r04.json",
-                  ("c3", "beam3", True): "traffic_decode_beam3_r05zh.json",
+TRAFFIC_DECODE = {("c3", "greedy", True): "traffic_decode_pl_r06q.json", ("c3", "greedy", False): "traffic_decode_chain_r06q.json",
+                  ("c3", "beam3", True): "traffic_decode_beam3_r06q.json",
                   ("c3", "beam3", False): "traffic_decode_beam3_r05f.json"}
-TRAFFIC_VOCODER = {"c3": "traffic_vocoder_r05zh.json"}
+TRAFFIC_VOCODER = {"c3": "traffic_vocoder_r06q.json"}
 
 
 class KernelTimer:

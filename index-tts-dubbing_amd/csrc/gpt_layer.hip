@@ -372,6 +372,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   // layers that can stay in the Infinity Cache; A = x^ tile 0), then the attention's first round of K/V rows
   // (pass 0), then the residual slices; the weight DMA goes out after the q/k/v sweep
   u32x4_t bw[4], av[4][2];
+  float uc0, uc1;  // the lane's c_attn fold terms (column lane % 16 of this workgroup's 12)
   // the residual slices (rows xrow of every tile, this thread's 2 columns), selected at phase D: no early wait
   float2 x_raw[MT];
 #pragma unroll
@@ -423,6 +424,12 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       for (int m = 1; m < 9; ++m) dma_one(w + 8 * m);
     }
   };
+  // pass 0's first valid key (its row's left padding), loaded once here: re-read at the pass (after the asm memory
+  // clobbers of the barriers, a fresh load) it was a vector load whose vmcnt(0) waited for phase A's granule and
+  // cache stores
+  // (one row tile only: at 96 beam rows beam3 measured 1172 -> 1183 us with it, r06q)
+  const int rr0 = NBM > 0 ? NBM * uib : (unit_row(0) < R ? unit_row(0) : 0);
+  const int p0_first = MT == 1 && p.pad ? p.pad[rr0] : 0;
   // the attention's first round of K/V rows (pass 0)
   auto kv_round0 = [&]() {
     if constexpr (NBM > 0) {
@@ -431,8 +438,8 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       kv_load_bm(kb, p.kc, p0, nk, 0);
       kv_load_bm(vb, p.vc, p0, nk, 0);
     } else {
-      const int r0 = unit_row(0), rr = r0 < R ? r0 : 0;
-      const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+      const int rr = rr0;
+      const int p0 = MT == 1 ? p0_first : (p.pad ? p.pad[rr] : 0), nk = kidx + 1 - p0;
       stage_kvi(rr, p0, nk);
       kv_load(kr, p.kc, rr, p0, nk, 0);
       kv_load(vr, p.vc, rr, p0, nk, 0);
@@ -450,8 +457,20 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
       for (int t = 0; t < NHF; ++t)
         av[i][t] = *reinterpret_cast<const u32x4_t*>(p.xh + (int64_t)(16 * t + c16) * kD + 32 * s + 8 * q4);
     }
+    // the lane's fold terms: one row tile (MT = 1) beside the operands (loaded in the epilogue, behind the K/V rows,
+    // it waited for the whole first K/V round, in-order vmcnt: C2 479 -> 473 us, C3 unchanged, r06p); row tiles
+    // > 1 behind the K/V rows (beside them beam3 measured 1174 -> 1185 us)
+    const int cq = (lane & 15) < kQC ? (lane & 15) : 0;
+    if constexpr (MT == 1) {
+      uc0 = Ly.qkv_uc[(int64_t)b * 2 * kQC + cq];
+      uc1 = Ly.qkv_uc[(int64_t)b * 2 * kQC + kQC + cq];
+    }
     __builtin_amdgcn_sched_barrier(0);
     kv_round0();
+    if constexpr (MT > 1) {
+      uc0 = Ly.qkv_uc[(int64_t)b * 2 * kQC + cq];
+      uc1 = Ly.qkv_uc[(int64_t)b * 2 * kQC + kQC + cq];
+    }
   }
 
   // fold statistics of one 32-row tile (the A fragments a wave accumulated): sums -> mu / rstd in LDS
@@ -488,14 +507,6 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
   // MFMAs (double-buffered; loaded inside the loop they were one serial round trip per tile: c_attn 8.8 us
   // at 3 tiles, profiles/pl_trace_r05q_96.txt)
   u32x4_t avn[4][2];
-  // the lane's fold terms (every row tile's), loaded ahead of the prefetches: an epilogue load behind them made
-  // the tile's stores wait for the next tile's A fragments (in-order vmcnt)
-  float uc0 = 0.f, uc1 = 0.f;
-  if constexpr (MT > 1) {
-    const int cq = (lane & 15) < kQC ? (lane & 15) : 0;
-    uc0 = Ly.qkv_uc[(int64_t)b * 2 * kQC + cq];
-    uc1 = Ly.qkv_uc[(int64_t)b * 2 * kQC + kQC + cq];
-  }
 #pragma unroll  // (MT > 1: straight-line tiles, so the compiler's vmcnt counts stay exact across them)
   for (int t = 0; t < MT; ++t) {
     if (MT > 1 && t + 1 < MT) {
@@ -562,8 +573,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
 #pragma unroll
         for (int ww = 0; ww < kNW; ++ww) v += red[(ww * 8 + e) * 64 + l];
         const int rt = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3), row = 32 * t + rt;
-        const float* uc = Ly.qkv_uc + (int64_t)b * 2 * kQC;
-        v = fold_apply(v, rsd[rt], mu[rt], uc[col], uc[kQC + col]);
+        v = fold_apply(v, rsd[rt], mu[rt], uc0, uc1);
         const int i = kQC * jj + col;  // index in head h's [q | k | v] 192 columns
         const uint64_t gr = ((uint64_t)L1 << 32) | __float_as_uint(v);
         __hip_atomic_store(gq + ((int64_t)row * kH + h) * 192 + i, gr, __ATOMIC_RELAXED, PL_SCOPE);
@@ -643,7 +653,7 @@ __global__ __launch_bounds__(kThreads) void gpt_layer_pl_kernel(PlArgs p) {
     const int r_u = unit_row(pt);
     const bool act_u = r_u < R;
     const int rr = act_u ? r_u : 0;
-    const int p0 = p.pad ? p.pad[rr] : 0, nk = kidx + 1 - p0;
+    const int p0 = MT == 1 ? p0_first : (p.pad ? p.pad[rr] : 0), nk = kidx + 1 - p0;
     if (pt > 0) {  // later passes: this pass's first round now
       stage_kvi(rr, p0, nk);
       kv_load(kr, p.kc, rr, p0, nk, 0);
