@@ -54,7 +54,7 @@ constexpr int kApTO = 32 * kApTiles - 64;  // conv outputs per job: 448; activat
 constexpr int kApWin = 32 * kApTiles + 32; // window rows: times t0 - 39 .. t0 + 504 (replicate-clamped)
 constexpr int kApPX = 64;                  // window row bytes: one 32-channel block (C <= 32)
 constexpr int kApKMax = 15;                // conv taps (odd, halo K / 2 <= 7 < 32)
-constexpr int kApLds = kApWin * kApPX + 128 + 32 * kApKMax * 4 + 32 * kApTiles * 32 * 2;
+constexpr int kApLds = kApWin * kApPX + 128 + 32 * kApKMax * 4 + 32 * kApTiles * 32 * 2 + 32 * kApKMax * 4;
 
 struct ApArgs {
   const uint16_t* x;
@@ -70,6 +70,8 @@ struct ApArgs {
   int64_t syb;
 };
 
+// CK = (C << 8) | K for a compile-time conv_post shape, 0 for the generic loop
+template <int CK>
 __global__ __launch_bounds__(256, 2) void act_post_conv_kernel(ApArgs p) {
   constexpr int PX = kApPX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -77,6 +79,7 @@ __global__ __launch_bounds__(256, 2) void act_post_conv_kernel(ApArgs p) {
   float* tl = reinterpret_cast<float*>(smem + kApWin * PX);             // 12 up, 12 down taps
   float* wl = tl + 32;                                                  // conv_post [C][K]
   uint16_t* at = reinterpret_cast<uint16_t*>(wl + 32 * kApKMax);        // activation rows [512][C] bf16
+  float* wt = reinterpret_cast<float*>(at + 32 * kApTiles * 32);        // conv_post tap-major [K][C] (CK > 0)
   const int b = blockIdx.y;
   const int len = p.lens ? p.lens[b] : p.T;
   const int t0 = blockIdx.x * kApTO;
@@ -86,6 +89,8 @@ __global__ __launch_bounds__(256, 2) void act_post_conv_kernel(ApArgs p) {
   const int C = p.C, K = p.K;
   if (tid < 24) tl[tid] = tid < 12 ? p.up[tid] : p.down[tid - 12];
   for (int i = tid; i < C * K; i += 256) wl[i] = p.w[i];
+  if constexpr (CK > 0)
+    for (int i = tid; i < C * K; i += 256) wt[(i % K) * C + i / K] = p.w[i];
   // window row r = time ta0 - 7 + r (clamped to [0, len)), channels >= C zero: the activation kernel's window
   const uint16_t* X = p.x + (int64_t)b * p.sxb;
   constexpr int NV = (kApWin * 4 + 255) / 256;
@@ -144,6 +149,56 @@ __global__ __launch_bounds__(256, 2) void act_post_conv_kernel(ApArgs p) {
   __syncthreads();
   // conv_post + tanh (+ int16): conv_post_tanh_kernel's loop order over the bf16 activation rows
   const int half = K / 2;
+  if constexpr (CK > 0) {
+    // compile-time C x K (BigVGAN2's conv_post: 24 x 7): tap j's C weights read once as 16-B vectors from a
+    // tap-major copy (wt) for both of the thread's outputs -- each output's fma chain (bias, then tap-major,
+    // channel inner) is the generic loop's below, which reads every weight with its own LDS load inside the
+    // chain: latency-bound, ~600 us of the 980 us launch at the C3 shape (bench_r06s_c3.json roofline_vocoder_tail).
+    constexpr int CC = CK >> 8, KK = CK & 255, HALF = KK / 2;
+    static_assert(CC % 8 == 0 && CC <= 32 && KK <= kApKMax, "conv_post shape");
+    float acc[2] = {p.bias, p.bias};
+    int ro[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = tid + 256 * q;
+      ro[q] = (o < kApTO ? o : 0) + 32 - HALF;  // activation row of tap 0 (t - half - ta0); clamped when idle
+    }
+#pragma unroll 1  // one tap's weights and rows live at a time (unrolled, the loads of every tap were hoisted: spills)
+    for (int j = 0; j < KK; ++j) {
+      float wj[CC];
+#pragma unroll
+      for (int c4 = 0; c4 < CC; c4 += 4) {
+        const f32x4_t w4 = *reinterpret_cast<const f32x4_t*>(wt + j * CC + c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wj[c4 + e] = w4[e];
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint16_t* row = at + (ro[q] + j) * CC;
+#pragma unroll
+        for (int c8 = 0; c8 < CC; c8 += 8) {
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(row + c8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t wv = v[e >> 1];
+            acc[q] = fmaf(wj[c8 + e], __uint_as_float((e & 1) ? (wv & 0xFFFF0000u) : (wv << 16)), acc[q]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = tid + 256 * q, t = t0 + o;
+      if (o >= kApTO || t >= len) continue;
+      const float v = tanhf(acc[q]);
+      if (p.wav) p.wav[(int64_t)b * p.syb + t] = v;
+      if (p.pcm) {
+        const float s = fminf(fmaxf(32767.0f * v, -32767.0f), 32767.0f);
+        p.pcm[(int64_t)b * p.syb + t] = (int16_t)s;
+      }
+    }
+    return;
+  }
   for (int o = tid; o < kApTO; o += 256) {
     const int t = t0 + o;
     if (t >= len) break;
@@ -185,7 +240,10 @@ extern "C" int itts_act_conv_post_tanh(const void* x, int64_t x_sb, int64_t ldx,
   ApArgs a{static_cast<const uint16_t*>(x), x_sb, ldx, up12, down12, log_alpha, log_beta, w, bias, C, K, lengths, Tmax,
            wav, pcm, y_sb};
   dim3 grid((Tmax + kApTO - 1) / kApTO, B);
-  hipLaunchKernelGGL(act_post_conv_kernel, grid, dim3(256), kApLds, itts::as_stream(stream), a);
+  if (C == 24 && K == 7)
+    hipLaunchKernelGGL(act_post_conv_kernel<(24 << 8) | 7>, grid, dim3(256), kApLds, itts::as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(act_post_conv_kernel<0>, grid, dim3(256), kApLds, itts::as_stream(stream), a);
   return itts::check_launch(fn);
 }
 
