@@ -25,6 +25,7 @@
 namespace {
 
 constexpr int kU = 8;
+constexpr int kNI = 4;  // decode_gemm16x: k-steps per wave of the straight-line form (K = 1024 at 8 waves)
 
 __device__ __forceinline__ float gelu_tanh_d(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
     for (int u = 0; u < kU; ++u)
       if (i0 + u < niter) dst[u] = ITTS_WLOAD(Wt + (int64_t)(w + NW * (i0 + u)) * 64);
   };
-  wload(wa, 0);
+  const bool straight = niter == kNI && kU >= kNI;  // wave-uniform
   f32x4_t acc[2 * MT];
   float ssum[2 * MT], ssq[2 * MT];  // FOLD: sums of the rows this lane holds (16-row half h: c16 + 16h)
 #pragma unroll
@@ -403,34 +404,58 @@ __global__ __launch_bounds__(64 * NW) void decode_gemm16x_kernel(Dg16xArgs p) {
     acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     ssum[t] = ssq[t] = 0.f;
   }
-  auto compute = [&](const u32x4_t (&src)[kU], int i0) {
+  auto aload = [&](bf16x8_t (&dst)[2 * MT], int kstep) __attribute__((always_inline)) {
+    const int64_t col = 32 * (w + NW * kstep) + 8 * q;
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      if (i0 + u >= niter) continue;
-      const int64_t col = 32 * (w + NW * (i0 + u)) + 8 * q;
-      bf16x8_t av[2 * MT];
+    for (int t = 0; t < 2 * MT; ++t) dst[t] = *reinterpret_cast<const bf16x8_t*>(A + (int64_t)(16 * t + c16) * p.lda + col);
+  };
+  auto step = [&](const bf16x8_t (&av)[2 * MT], const u32x4_t& wsrc) __attribute__((always_inline)) {
+    const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&wsrc);
 #pragma unroll
-      for (int t = 0; t < 2 * MT; ++t) av[t] = *reinterpret_cast<const bf16x8_t*>(A + (int64_t)(16 * t + c16) * p.lda + col);
-      const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(&src[u]);
+    for (int t = 0; t < 2 * MT; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[t], bfr, acc[t], 0, 0, 0);
+      if constexpr (FOLD) {
 #pragma unroll
-      for (int t = 0; t < 2 * MT; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[t], bfr, acc[t], 0, 0, 0);
-        if constexpr (FOLD) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = (float)av[t][e];
-            ssum[t] += v;
-            ssq[t] = fmaf(v, v, ssq[t]);
-          }
+        for (int e = 0; e < 8; ++e) {
+          const float v = (float)av[t][e];
+          ssum[t] += v;
+          ssq[t] = fmaf(v, v, ssq[t]);
         }
       }
     }
   };
+  auto compute = [&](const u32x4_t (&src)[kU], int i0) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (i0 + u >= niter) continue;
+      bf16x8_t av[2 * MT];
+      aload(av, i0 + u);
+      step(av, src[u]);
+    }
+  };
+  if (straight) {
+    // K = 32 kNI NW (1024 at NW = 8): straight-line k-steps, k-step u + 1's A fragments requested before k-step
+    // u's MFMAs (requested right before them, every k-step paid a full L2 round trip: 12.5 us per 128-row launch
+    // in the C5 chain, profiles/kernel_stats_c5_r06r.txt); the same values in the same order: bit-identical
+    u32x4_t wf[kNI];  // the wave's kNI weight fragments, loaded unconditionally
+#pragma unroll
+    for (int u = 0; u < kNI; ++u) wf[u] = ITTS_WLOAD(Wt + (int64_t)(w + NW * u) * 64);
+    bf16x8_t a0[2 * MT], a1[2 * MT];
+    aload(a0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kNI; ++u) {
+      if (u + 1 < kNI) aload((u & 1) ? a0 : a1, u + 1);
+      step((u & 1) ? a1 : a0, wf[u]);
+    }
+  } else {
+  wload(wa, 0);
   for (int i0 = 0; i0 < niter; i0 += 2 * kU) {
     if (i0 + kU < niter) wload(wb, i0 + kU);
     compute(wa, i0);
     if (i0 + 2 * kU < niter) wload(wa, i0 + 2 * kU);
     if (i0 + kU < niter) compute(wb, i0 + kU);
+  }
   }
   if constexpr (FOLD) {
 #pragma unroll
