@@ -503,9 +503,10 @@ int itts_gpt_pl_reset(void* scratch, void* stream);
  * the mlp.c_proj reduce (+ ln_f + final_norm) to itts_residual_reduce_ln over the scratch partials. */
 int itts_gpt_layer_pl(const ItTsGptLayerW* layer_w, const ItTsGptPlLayerW* pl, const ItTsGptDecodeState* state,
                       int layer, int kstep, int last, void* scratch, void* stream);
-/* A hand-off timeout recorded in the scratch (0 = none; else every later layer launch returns at once
- * and the results are invalid until itts_gpt_pl_reset; the launch chain, itts_gpt_decode_steps, gives
- * the same results bit for bit and needs no scratch).  Synchronises `stream`. */
+/* A hand-off timeout recorded in the scratch (0 = none; else every later layer launch runs only its c_attn
+ * phase and returns at its q/k/v sweep, without polling -- a few microseconds, so the rest of a graph replay
+ * drains quickly -- and the results are invalid until itts_gpt_pl_reset; the launch chain,
+ * itts_gpt_decode_steps, gives the same results bit for bit and needs no scratch).  Synchronises `stream`. */
 int itts_gpt_pl_error(const void* scratch, void* stream, int* code);
 /* itts_gpt_decode_steps with every layer on the persistent path (pl: [n_layer]); sampling mode 2 (beams:
  * logits only, nsteps = 1, the caller runs the beam kernels and the step advance) as itts_gpt_decode_step. */
