@@ -845,7 +845,7 @@ class HipGPT:
             ln = self._lane(i, r1 - r0, max_new_tokens, s)
             if ln["st"].get("multi_lane", False) != (len(bounds) > 1):
                 ln["st"]["multi_lane"] = len(bounds) > 1
-                ln["graph"] = ln["multi"] = None  # captured for the other decode path
+                self._drop_graphs(ln)  # captured for the other decode path
             ln["stream"].wait_stream(main)  # inputs prepared on the caller's stream
             with torch.cuda.stream(ln["stream"]):
                 self._start_lane(ln, emb[r0:r1], pad[r0:r1], s, r0, sampling, seed,
@@ -924,12 +924,12 @@ class HipGPT:
             fc[:, : forced.shape[1]] = forced.to(self.dev, torch.int32)
             if st.get("forced") is None:
                 st["forced"] = fc
-                ln["graph"] = ln["multi"] = None  # both graphs hold the forced-codes pointer
+                self._drop_graphs(ln)  # every graph holds the forced-codes pointer
             else:
                 st["forced"].copy_(fc)
         elif st.get("forced") is not None:
             st["forced"] = None
-            ln["graph"] = ln["multi"] = None
+            self._drop_graphs(ln)
         # ---- prefill over [B, s+1] rows ----
         M = B * (s + 1)
         x = emb.reshape(M, self.D).contiguous()
@@ -963,9 +963,33 @@ class HipGPT:
             self.logits_trace.append(st["logits"][:, : self.V].clone())
         ln["graph_ok"] = False
         if use_graph:
-            if ln["graph"] is None or ln["graph"][1] != gkey:
-                ln["graph"] = (self._capture(st, min_new, penalty), gkey)
+            ln["graph"] = (self._cached_graph(ln, gkey, lambda: self._capture(st, min_new, penalty)), gkey)
             ln["graph_ok"] = True
+
+    # captured graphs kept per lane, keyed by what they were captured for (one-step and multi-step graphs of the
+    # persistent layers and of the launch chain): synthesize_many's overlap alternates between the two decode paths
+    # for the same shape, which recaptured at every switch with one slot per lane
+    GRAPH_CACHE = 4
+
+    def _keep_graph(self, ln, key, g):
+        cache = ln.setdefault("graphs", {})
+        cache.pop(key, None)
+        cache[key] = g
+        while len(cache) > self.GRAPH_CACHE:
+            cache.pop(next(iter(cache)))  # oldest first
+
+    def _cached_graph(self, ln, gkey, capture):
+        cache = ln.setdefault("graphs", {})
+        g = cache.get(("one", gkey))
+        if g is None:
+            g = capture()
+        self._keep_graph(ln, ("one", gkey), g)
+        return g
+
+    @staticmethod
+    def _drop_graphs(ln):
+        ln["graph"] = ln["multi"] = None
+        ln["graphs"] = {}
 
     MUTABLE = ("t", "x", "h", "seen", "done", "codes")
     BEAM_MUTABLE = ("beam_score", "kv_rows", "done_u", "hyp_score", "hyp_len", "hyp_codes", "hyp_n", "hyp_order",
@@ -981,21 +1005,27 @@ class HipGPT:
     def _multi_graph(self, ln, n, min_new, penalty, gkey):
         """the lane's n-step graph (captured on first use, like the one-step graph)."""
         mg = ln.get("multi")
-        if mg is None or mg[1] != (n, gkey):
-            st = ln["st"]
-            keys = self.MUTABLE + (self.BEAM_MUTABLE if "kv_rows" in st else ())
-            saved = {k: st[k].clone() for k in keys}
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                if self.cstep and "kv_rows" not in st:  # n steps, one counter advance
-                    self._decode_step_c(st, min_new, penalty, nsteps=n)
-                else:
-                    for _ in range(n):
-                        self._decode_step(st, min_new, penalty)
-            for k, v in saved.items():
-                st[k].copy_(v)
-            mg = ln["multi"] = (g, (n, gkey))
-        return mg[0]
+        if mg is not None and mg[1] == (n, gkey):
+            return mg[0]
+        cached = ln.setdefault("graphs", {}).get(("multi", n, gkey))
+        if cached is not None:
+            ln["multi"] = (cached, (n, gkey))
+            return cached
+        st = ln["st"]
+        keys = self.MUTABLE + (self.BEAM_MUTABLE if "kv_rows" in st else ())
+        saved = {k: st[k].clone() for k in keys}
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            if self.cstep and "kv_rows" not in st:  # n steps, one counter advance
+                self._decode_step_c(st, min_new, penalty, nsteps=n)
+            else:
+                for _ in range(n):
+                    self._decode_step(st, min_new, penalty)
+        for k, v in saved.items():
+            st[k].copy_(v)
+        self._keep_graph(ln, ("multi", n, gkey), g)
+        ln["multi"] = (g, (n, gkey))
+        return g
 
     def _capture(self, st, min_new, penalty):
         """Capture one decode step into a hipGraph; counters are device-side so replays advance."""
@@ -1144,7 +1174,8 @@ class HipGPT:
         gkey = (K, min_new_tokens, repetition_penalty, length_penalty, sampling, self.cstep, self.pl_active)
         graph_ok = use_graph and max_new_tokens > 1
         if graph_ok and (ln["graph"] is None or ln["graph"][1] != gkey):
-            ln["graph"] = (self._capture(st, min_new_tokens, repetition_penalty), gkey)
+            ln["graph"] = (self._cached_graph(ln, gkey, lambda: self._capture(st, min_new_tokens, repetition_penalty)),
+                           gkey)
         steps = 1
         ev = self.step_events  # optional instrumentation (bench.py): HIP events around each step
         # distinct cache keys a step reads: each utterance's prompt once (shared by its beams through
