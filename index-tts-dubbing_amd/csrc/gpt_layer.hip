@@ -11,11 +11,11 @@
 //   workgroup b = 8 j + c: cluster c = b % 8 (round-robin dispatch puts a cluster on one XCD: a speed
 //   assumption only, never a correctness one), index j in the cluster.  Cluster c owns heads 2c, 2c+1,
 //   c_fc columns [512c, 512c+512) and K range [512c, 512c+512) of mlp.c_proj (= split s of the chain's
-//   split-K 8), and k-steps [128c, 128c+128) of attn.c_proj (its split c).  8 waves; right after its
-//   c_attn operands and K/V rows, each wave requests 1/8 of this workgroup's attn.c_proj / c_fc /
-//   mlp.c_proj weights (72 KiB) into LDS by LDS-DMA, so the weights of the later phases stream while
-//   the early phases and their hand-offs run.  (A dedicated 9th loader wave cost 3 waves per SIMD =
-//   168 VGPRs and spilled.)
+//   split-K 8), and k-steps [128c, 128c+128) of attn.c_proj (its split c).  8 waves; after the q/k/v
+//   sweep each wave requests 1/8 of this workgroup's attn.c_proj slice (8 KiB) into LDS by LDS-DMA, and
+//   after the E2 add 1/8 of its c_fc / mlp.c_proj slices (64 KiB, round 6: issued with the attention,
+//   the first key round waited for them), so the weights of the later phases stream while the hand-offs
+//   run.  (A dedicated 9th loader wave cost 3 waves per SIMD = 168 VGPRs and spilled.)
 //   A  c_attn (ln_1 folded): 12 columns of head h = 2c + j/16 (3072 / 256), A = x^ (previous launch).
 //      The attention waves request their first round of K/V rows BEFORE this phase's MFMAs.
 //   E1 q/k/v -> attention: 8-byte {tag, value} granules (the data is the flag: no drain, so the K/V
