@@ -40,10 +40,10 @@ PEAK_HBM_GBS = 8000.0
 # per decoding and decode path (persistent layers or the launch chain): None until measured for this build
 # PMC files are measured on the C3 workload (profiles/pmc_decode.py, pmc_vocoder.py): other workloads report
 # traffic null rather than C3's bytes
-TRAFFIC_DECODE = {("c3", "greedy", True): "traffic_decode_pl_r06q.json", ("c3", "greedy", False): "traffic_decode_chain_r06q.json",
-                  ("c3", "beam3", True): "traffic_decode_beam3_r06q.json",
+TRAFFIC_DECODE = {("c3", "greedy", True): "traffic_decode_pl_r06y.json", ("c3", "greedy", False): "traffic_decode_chain_r06y.json",
+                  ("c3", "beam3", True): "traffic_decode_beam3_r06y.json",
                   ("c3", "beam3", False): "traffic_decode_beam3_r05f.json"}
-TRAFFIC_VOCODER = {"c3": "traffic_vocoder_r06q.json"}
+TRAFFIC_VOCODER = {"c3": "traffic_vocoder_r06y.json"}
 
 
 class KernelTimer:
