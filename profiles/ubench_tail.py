@@ -58,3 +58,11 @@ for B in (32, 1):
                                                  ctypes.c_float(10.0), P(emb.data_ptr()), P(pos.data_ptr()), 0, K, None,
                                                  None, P(x.data_ptr()), P(h.data_ptr()), 1, B, None, P(s)), "se")
     print(f"sample_embed B={B:2d}: {timeit(f):7.2f} us")
+    f0 = lambda: _hip.check(lib.itts_sample_embed(P(logits.data_ptr()), ldl, V, P(seen.data_ptr()), P(done.data_ptr()),
+                                                  P(codes.data_ptr()), 1024, P(tstate.data_ptr()), 0, 0, 8193,
+                                                  ctypes.c_float(10.0), None, None, 0, K, None, None, None, None, 1, B,
+                                                  None, P(s)), "se0")
+    print(f"sample (no embedding) B={B:2d}: {timeit(f0):7.2f} us")
+    z = torch.zeros(1, device=dev)
+    fz = lambda: z.add_(1.0)
+    print(f"empty elementwise launch: {timeit(fz):7.2f} us")
