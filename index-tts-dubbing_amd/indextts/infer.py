@@ -258,7 +258,14 @@ class IndexTTS:
         min_new_tokens = kw.pop("min_new_tokens", 0)
         seed = kw.pop("seed", None)
         kw.pop("num_return_sequences", None)
-        if kw:  # e.g. inference_speech's typical_sampling / typical_mass (gpt/model.py:655-708; off by default)
+        # inference_speech's own defaults (gpt/model.py:655-656): typical sampling off (typical_mass then unused) and
+        # HF generate's use_cache=True are what the HIP decode does anyway; only the settings it cannot honour warn
+        if not kw.get("typical_sampling", False):
+            kw.pop("typical_sampling", None)
+            kw.pop("typical_mass", None)
+        if kw.get("use_cache", True):
+            kw.pop("use_cache", None)
+        if kw:  # e.g. typical_sampling=True, no_repeat_ngram_size (gpt/model.py:655-708 -> HF generate)
             warnings.warn(f"ignored generation kwargs: {sorted(kw)} -- the HIP decode honours do_sample, top_p, "
                           "top_k, temperature, length_penalty, num_beams, repetition_penalty, max_mel_tokens, "
                           "min_new_tokens, seed (INTEGRATION.md §2); the reference would pass the rest to "

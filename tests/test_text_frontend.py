@@ -153,6 +153,15 @@ def test_decoding_kwargs():
     assert (s["top_k"], s["top_p"], "num_beams" in s) == (0, 0.5, False)
     s = IndexTTS._decoding(dict(do_sample=True, num_beams=3, top_k=200))
     assert (s["top_k"], s["num_beams"]) == (200, 3)
+    # inference_speech's defaults passed explicitly are no-ops (no warning); settings the decode cannot honour warn
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert IndexTTS._decoding(dict(typical_sampling=False, typical_mass=0.9, use_cache=True)) == d
+    assert not w
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        IndexTTS._decoding(dict(typical_sampling=True, typical_mass=0.5))
+    assert any("typical_mass" in str(x.message) and "typical_sampling" in str(x.message) for x in w)
 
 
 def test_cli_argument_checks(tmp_path, capsys):
